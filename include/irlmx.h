@@ -1,0 +1,181 @@
+/*
+ * irlmx -- MI355X-native MaxEnt-IRL inner loop: C ABI of libirlmx.so.
+ *
+ * The reference (narendasan/irl-maxent) has no FFI: its hot path is a set of
+ * module-level numpy functions in src/maxent.py and src/solver.py that
+ * src/main.py imports as `import maxent as M`, `import solver as S`
+ * (main.py:4, 7).  Each entry point below replaces the numeric core of one of
+ * those functions; the Python drop-in modules (irl-maxent_amd/maxent.py,
+ * irl-maxent_amd/solver.py) keep the reference's names, signatures and return
+ * types and call these through ctypes.
+ *
+ * Conventions
+ *  - Every array pointer is a caller-owned DEVICE buffer (e.g. a torch tensor's
+ *    data_ptr()); the library allocates nothing.  `stream` is a hipStream_t.
+ *  - Instances: B independent problems are processed per call.  Per-instance
+ *    arrays are packed [B][...] in the layouts stated per argument.
+ *  - Return value: IRLMX_SUCCESS (0) or a negative IRLMX_E* code; the message
+ *    of the last failure on this thread is irlmx_last_error().
+ *  - Per-instance outcome codes (IRLMX_OK / _NONFINITE / _MAXITER) are written
+ *    to `status`, and the number of sweeps each fixed-point loop ran to
+ *    `iterations` -- the count of iterations of the reference's `while` loop.
+ *  - Work is enqueued on `stream`.  Calls whose sweep count is data dependent
+ *    and that do not fit one workgroup per instance (large state spaces)
+ *    synchronise `stream` while they run; all others are fully asynchronous.
+ *  - Arithmetic is IEEE float64 throughout, as in the reference.
+ */
+#ifndef IRLMX_H
+#define IRLMX_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define IRLMX_ABI_VERSION 1
+
+/* transition-table layouts (see irlmx_mdp) */
+#define IRLMX_LAYOUT_STENCIL5 1 /* grid-local: self, +x, -x, +y, -y on a width x height grid */
+#define IRLMX_LAYOUT_ELL 2      /* generic sparse: k_row target slots per state */
+
+/* return codes */
+#define IRLMX_SUCCESS 0
+#define IRLMX_EINVAL (-1)
+#define IRLMX_EHIP (-2)
+#define IRLMX_EWORKSPACE (-3)
+
+/* per-instance status */
+#define IRLMX_OK 0
+#define IRLMX_NONFINITE 1 /* a NaN stopped the loop (the reference's `while delta > eps` exits on NaN) */
+#define IRLMX_MAXITER 2   /* stopped by the optional sweep cap before convergence */
+
+/* workspace owners (irlmx_workspace_bytes) */
+#define IRLMX_OP_BACKWARD 1
+#define IRLMX_OP_FORWARD 2
+#define IRLMX_OP_SOFT_BACKWARD 3
+#define IRLMX_OP_VALUE_ITERATION 4
+
+/*
+ * Transition model P[from, to, action] of B instances (the reference's dense
+ * `p_transition`, gridworld.py:124-142), stored compactly in HBM.
+ *
+ *  row form  (used by the backward passes and value iteration):
+ *    row_val[b'][a][k][s] = P[s, target_k(s), a]       (float64)
+ *    STENCIL5: target_k(s) is the k-th stencil neighbour of s; row_idx unused.
+ *    ELL     : target_k(s) = row_idx[b'][k][s]; unused slots have value 0.
+ *  column form (used by the forward SVF pass, ELL only; STENCIL5 derives it):
+ *    col_idx[b'][k][t] = source state s of slot k of target t,
+ *    col_val[b'][a][k][t] = P[s, t, a].
+ *  b' = 0 when `shared` is nonzero (one table for all B instances), else b.
+ */
+typedef struct irlmx_mdp {
+  int32_t layout;
+  int32_t n_states;
+  int32_t n_actions;
+  int32_t width;  /* STENCIL5 only */
+  int32_t height; /* STENCIL5 only */
+  int32_t k_row;  /* slots per state in the row form (5 for STENCIL5) */
+  int32_t k_col;  /* slots per state in the column form (ELL) */
+  int32_t batch;
+  int32_t shared;
+  int32_t reserved;
+  const double* row_val;
+  const int32_t* row_idx;
+  const int32_t* col_idx;
+  const double* col_val;
+} irlmx_mdp;
+
+int irlmx_abi_version(void);
+const char* irlmx_last_error(void);
+
+/* Bytes of device workspace `op` needs for this model (0 is a valid answer). */
+size_t irlmx_workspace_bytes(const irlmx_mdp* mdp, int32_t op);
+
+/*
+ * Non-causal MaxEnt backward pass -- replaces the numeric core of
+ * maxent.local_action_probabilities (reference src/maxent.py:119-159).
+ *   reward   [B][S]     per-state reward r (the reference's `reward`)
+ *   terminal [B][S]     1 for terminal states (zs[terminal] = 1, maxent.py:147)
+ *   rescale  nonzero: multiply the partition vector by a power of two each sweep
+ *            (ratio-preserving; keeps it finite where the reference overflows)
+ *   p_action [B][S][A]  out: za / zs after exactly 2*S sweeps
+ */
+int irlmx_backward_maxent(const irlmx_mdp* mdp, const double* reward, const uint8_t* terminal,
+                          int32_t rescale, double* p_action, int32_t* status, void* workspace,
+                          size_t workspace_bytes, void* stream);
+
+/*
+ * Forward expected-SVF sweep -- replaces maxent.expected_svf_from_policy
+ * (reference src/maxent.py:63-114): d <- p0 + sum_a P'_a^T (pi_a * d) from d = 0
+ * until max|delta| <= eps, where P' has the terminal rows cleared.
+ *   p_initial [B][S], terminal [B][S] (uint8), p_action [B][S][A]
+ *   max_iter  <= 0: unbounded, like the reference
+ *   svf [B][S] out; iterations [B] out (int64); status [B] out
+ */
+int irlmx_forward_svf(const irlmx_mdp* mdp, const double* p_initial, const uint8_t* terminal,
+                      const double* p_action, double eps, int64_t max_iter, double* svf,
+                      int64_t* iterations, int32_t* status, void* workspace,
+                      size_t workspace_bytes, void* stream);
+
+/*
+ * MaxCausalEnt soft value iteration -- replaces
+ * maxent.local_causal_action_probabilities (reference src/maxent.py:279-341).
+ *   reward [B][S]; terminal_reward [B][S] = phi (-inf except 0 at terminals, or
+ *   the caller's phi vector, maxent.py:313-317); discount = gamma
+ *   p_action [B][S][A] out = exp(q - v); value [B][S] out = v (may be NULL)
+ */
+int irlmx_soft_backward(const irlmx_mdp* mdp, const double* reward, const double* terminal_reward,
+                        double discount, double eps, int64_t max_iter, double* p_action,
+                        double* value, int64_t* iterations, int32_t* status, void* workspace,
+                        size_t workspace_bytes, void* stream);
+
+/*
+ * Value iteration -- replaces solver.value_iteration (average = 0, reference
+ * src/solver.py:9-52) and solver.stochastic_value_iteration (average != 0,
+ * src/solver.py:55-104).   value [B][S] out.
+ */
+int irlmx_value_iteration(const irlmx_mdp* mdp, const double* reward, double discount, double eps,
+                          int32_t average, int64_t max_iter, double* value, int64_t* iterations,
+                          int32_t* status, void* workspace, size_t workspace_bytes, void* stream);
+
+/*
+ * Policy extraction from a value function -- replaces
+ * solver.optimal_policy_from_value (src/solver.py:107-124: argmax over the
+ * values of the intended successors, first index on ties and NaN counted as
+ * the maximum, as np.argmax) and solver.stochastic_policy_from_value
+ * (src/solver.py:155-181: weighted successor values normalised per state).
+ *   successor [S][A] (int32, shared by all instances): intended next state of
+ *     (s, a), i.e. world.state_index_transition(s, a) (gridworld.py:105-122)
+ *   value [B][S] -> policy [B][S] (int64)
+ *   weighted_value [B][S] = w(value) elementwise -> p_policy [B][S][A]
+ */
+int irlmx_optimal_policy(const int32_t* successor, int32_t n_states, int32_t n_actions, int32_t batch,
+                         const double* value, int64_t* policy, void* stream);
+int irlmx_stochastic_policy(const int32_t* successor, int32_t n_states, int32_t n_actions, int32_t batch,
+                            const double* weighted_value, double* p_policy, void* stream);
+
+/*
+ * World builders -- replace the O(S^2 A) Python constructors of
+ * gridworld.IcyGridWorld / gridworld.GridWorld (src/gridworld.py:124-248),
+ * emitting the STENCIL5 row form directly, bit-identical values.
+ *   p_slip [B] (device), row_val [B][4][5][S] out (device)
+ */
+int irlmx_build_icy_gridworld(int32_t size, const double* p_slip, int32_t batch, double* row_val,
+                              void* stream);
+int irlmx_build_gridworld(int32_t size, int32_t batch, double* row_val, void* stream);
+
+/*
+ * Dense [S][S][A] float64 table (device) -> STENCIL5 row form on a width x height
+ * grid.  *off_stencil (device int32) is set nonzero when some nonzero entry is
+ * not a stencil neighbour (the table then needs the ELL layout).
+ */
+int irlmx_dense_to_stencil(const double* dense, int32_t width, int32_t height, int32_t n_actions,
+                           double* row_val, int32_t* off_stencil, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* IRLMX_H */

@@ -1,0 +1,978 @@
+// Fixed-point sweeps of the MaxEnt-IRL inner loop on gfx950.
+//
+//   backward  (maxent.py:119-159)  zs <- exp(r) * sum_a P_a zs, 2*S sweeps, then za/zs
+//   forward   (maxent.py:63-114)   d  <- p0 + sum_a P'_a^T (pi_a * d) until max|dd| <= eps
+//   soft VI   (maxent.py:279-341)  v  <- fold_a softmax(v, r + g P_a v) until max|dv| <= eps
+//   VI        (solver.py:9-104)    v  <- r + max_a / mean_a (g P_a v) until max|dv| <= eps
+//
+// Two execution shapes, chosen per call from the state count S:
+//
+//  * fused: one workgroup owns one instance for the WHOLE loop.  The two
+//    ping-pong state vectors live in LDS (2*S*8 B <= 64 KiB at S = 4096), each
+//    thread keeps the weights and neighbour indices of its SPT states in
+//    registers, and a sweep costs one workgroup barrier: the convergence test
+//    max|new - old| is a wave shuffle-max plus one LDS atomic max into a
+//    3-slot ring, so there is no host round trip until the loop has converged.
+//  * sweep: S too large for one CU.  One launch per sweep over all B
+//    instances; vectors in HBM, per-instance max|delta| by one global atomic
+//    per workgroup into a 3-slot ring, and a per-instance done flag that
+//    freezes an instance once converged, so the host can enqueue sweeps in
+//    chunks and only polls a done counter between chunks.
+//
+// The convergence word is the raw bits of |x| as uint64: for non-negative
+// doubles integer order is numeric order and NaN sorts above +inf, so the
+// integer max reproduces np.max(np.abs(.)) including NaN propagation, and
+// `!(delta > eps)` stops on NaN exactly like the reference's `while delta > eps`.
+
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <vector>
+
+#include "common.h"
+
+namespace irlmx {
+
+void set_error(const char* fmt, ...);
+int hip_fail(hipError_t e, const char* what);
+
+constexpr int kFusedMaxStates = 4096;
+
+// Largest S run by the fused shape; IRLMX_FUSED_MAX_STATES lowers it (tests use
+// 0 to drive every size through the sweep shape).
+static int fused_max_states() {
+  const char* e = getenv("IRLMX_FUSED_MAX_STATES");
+  if (!e || !*e) return kFusedMaxStates;
+  const int v = atoi(e);
+  return v < kFusedMaxStates ? v : kFusedMaxStates;
+}
+constexpr int kMaxActions = 8;
+constexpr int kSweepThreads = 256;
+
+// ---------------------------------------------------------------------------
+// model views
+// ---------------------------------------------------------------------------
+
+struct Model {
+  int S, A, K, W, H, B, stencil, shared, Kc;
+  const double* row_val;
+  const int32_t* row_idx;
+  const int32_t* col_idx;
+  const double* col_val;
+};
+
+static Model make_model(const irlmx_mdp* m) {
+  Model o;
+  o.S = m->n_states;
+  o.A = m->n_actions;
+  o.stencil = m->layout == IRLMX_LAYOUT_STENCIL5;
+  o.K = o.stencil ? kStencilK : m->k_row;
+  o.Kc = o.stencil ? kStencilK : m->k_col;
+  o.W = m->width;
+  o.H = m->height;
+  o.B = m->batch;
+  o.shared = m->shared != 0;
+  o.row_val = m->row_val;
+  o.row_idx = m->row_idx;
+  o.col_idx = m->col_idx;
+  o.col_val = m->col_val;
+  return o;
+}
+
+__device__ inline size_t inst_of(const Model& m, int b) { return m.shared ? 0 : (size_t)b; }
+
+// neighbour (row form) of s in slot k
+__device__ inline int row_nbr(const Model& m, int b, int s, int k) {
+  if (m.stencil) return stencil_nbr(s, k, m.W, m.H);
+  return m.row_idx[(inst_of(m, b) * m.K + k) * m.S + s];
+}
+
+__device__ inline double row_val(const Model& m, int b, int a, int k, int s) {
+  return m.row_val[((inst_of(m, b) * m.A + a) * m.K + k) * m.S + s];
+}
+
+// source (column form) of target t in slot k
+__device__ inline int col_src(const Model& m, int b, int t, int k) {
+  if (m.stencil) return stencil_nbr(t, k, m.W, m.H);
+  return m.col_idx[(inst_of(m, b) * m.Kc + k) * m.S + t];
+}
+
+// ---------------------------------------------------------------------------
+// workspace carving
+// ---------------------------------------------------------------------------
+
+struct Ws {
+  double* wgt;                // forward: [B][Kc][S] gather weights; backward: [B'][K][S]
+  int32_t* bad;               // [B] forward: policy has a non-finite entry
+  double* buf0;               // [B][S]   sweep path ping
+  double* buf1;               // [B][S]   sweep path pong
+  unsigned long long* slots;  // [B][3]
+  int32_t* done;              // [B]
+  int64_t* iters;             // [B]
+  int32_t* ndone;             // [1]
+  size_t total;
+};
+
+static size_t align256(size_t x) { return (x + 255) & ~size_t(255); }
+
+static bool use_fused(const Model& m, int op);
+
+static Ws carve(const Model& m, int op, void* base) {
+  Ws w;
+  size_t off = 0;
+  char* p = (char*)base;
+  auto take = [&](size_t bytes) {
+    char* r = p ? p + off : nullptr;
+    off += align256(bytes);
+    return (void*)r;
+  };
+  const size_t B = m.B, S = m.S;
+  size_t nw = 0;
+  if (op == IRLMX_OP_FORWARD) nw = B * m.Kc * S;
+  if (op == IRLMX_OP_BACKWARD) nw = (m.shared ? 1 : B) * m.K * S;
+  w.wgt = (double*)take(nw * sizeof(double));
+  w.bad = (int32_t*)take(B * sizeof(int32_t));
+  const bool sweep = !use_fused(m, op);
+  w.buf0 = (double*)take(sweep ? B * S * sizeof(double) : 0);
+  w.buf1 = (double*)take(sweep ? B * S * sizeof(double) : 0);
+  w.slots = (unsigned long long*)take(B * 3 * sizeof(unsigned long long));
+  w.done = (int32_t*)take(B * sizeof(int32_t));
+  w.iters = (int64_t*)take(B * sizeof(int64_t));
+  w.ndone = (int32_t*)take(sizeof(int32_t) * 4);
+  w.total = off;
+  return w;
+}
+
+// ---------------------------------------------------------------------------
+// weight preparation
+// ---------------------------------------------------------------------------
+
+// Gather weights of the forward pass, one per (target t, slot k):
+//   w[k][t] = sum_a P[s, t, a] * pi[s, a]  over non-terminal sources s = src_k(t)
+// (P' of maxent.py:98-99 has the terminal rows cleared).  Any non-finite
+// policy entry makes the reference's dense dgemv return NaN everywhere after
+// one sweep (0 * NaN inside the dot), so such instances are flagged in `bad`.
+__global__ void fwd_weights_kernel(Model m, const double* __restrict__ pi,
+                                   const uint8_t* __restrict__ term, double* __restrict__ w,
+                                   int32_t* __restrict__ bad) {
+  const int t = blockIdx.x * blockDim.x + threadIdx.x;
+  const int b = blockIdx.y;
+  if (t >= m.S) return;
+  const int S = m.S, A = m.A;
+  const double* pib = pi + (size_t)b * S * A;
+  const uint8_t* tb = term + (size_t)b * S;
+  bool nonfinite = false;
+  for (int a = 0; a < A; ++a) nonfinite |= !isfinite(pib[(size_t)t * A + a]);
+  for (int k = 0; k < m.Kc; ++k) {
+    double acc = 0.0;
+    if (m.stencil) {
+      if (stencil_valid(t, k, m.W, m.H)) {
+        const int s = stencil_nbr(t, k, m.W, m.H);
+        const int kk = stencil_opposite(k);  // direction from s back to t
+        if (!tb[s])
+          for (int a = 0; a < A; ++a) acc = fma(row_val(m, b, a, kk, s), pib[(size_t)s * A + a], acc);
+      }
+    } else {
+      const int s = col_src(m, b, t, k);
+      if (!tb[s]) {
+        const size_t base = inst_of(m, b) * A;
+        for (int a = 0; a < A; ++a)
+          acc = fma(m.col_val[((base + a) * m.Kc + k) * S + t], pib[(size_t)s * A + a], acc);
+      }
+    }
+    w[((size_t)b * m.Kc + k) * S + t] = acc;
+  }
+  if (nonfinite) atomicOr(&bad[b], 1);
+}
+
+// Collapsed backward weights: sum_a P[s, target_k(s), a] (reward independent).
+__global__ void bwd_weights_kernel(Model m, double* __restrict__ w) {
+  const int s = blockIdx.x * blockDim.x + threadIdx.x;
+  const int bi = blockIdx.y;  // table instance
+  if (s >= m.S) return;
+  for (int k = 0; k < m.K; ++k) {
+    double acc = 0.0;
+    for (int a = 0; a < m.A; ++a)
+      acc += m.row_val[(((size_t)bi * m.A + a) * m.K + k) * m.S + s];
+    w[((size_t)bi * m.K + k) * m.S + s] = acc;
+  }
+}
+
+// ---------------------------------------------------------------------------
+// fused (one workgroup per instance) kernels
+// ---------------------------------------------------------------------------
+
+struct FwdArgs {
+  Model m;
+  const double* w;  // [B][Kc][S]
+  const int32_t* bad;
+  const double* p0;
+  double eps;
+  long long max_iter;
+  double* out;
+  int64_t* iters;
+  int32_t* status;
+};
+
+__device__ inline int finish_status(double delta, double eps) {
+  if (delta != delta) return IRLMX_NONFINITE;
+  return delta > eps ? IRLMX_MAXITER : IRLMX_OK;
+}
+
+// one barrier per sweep; LDS: two S-vectors + 3 convergence slots
+template <int SPT, int KMAX>
+__global__ void __launch_bounds__(1024) fwd_fused_kernel(FwdArgs a) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  const Model& m = a.m;
+  const int S = m.S, K = m.Kc;
+  const int b = blockIdx.x, tid = threadIdx.x, nt = blockDim.x;
+  double* bufA = (double*)smem;
+  double* bufB = bufA + S;
+  unsigned long long* slot = (unsigned long long*)(bufB + S);
+
+  if (a.bad[b]) {  // non-finite policy: the reference yields NaN after one sweep
+    for (int s = tid; s < S; s += nt) a.out[(size_t)b * S + s] = __longlong_as_double(0x7ff8000000000000LL);
+    if (tid == 0) { a.iters[b] = 1; a.status[b] = IRLMX_NONFINITE; }
+    return;
+  }
+
+  double w[SPT][KMAX];
+  int nb[SPT][KMAX];
+  double p0[SPT], cur[SPT];
+  const double* wb = a.w + (size_t)b * K * S;
+#pragma unroll
+  for (int j = 0; j < SPT; ++j) {
+    const int s = tid + j * nt;
+    cur[j] = 0.0;
+    p0[j] = 0.0;
+#pragma unroll
+    for (int k = 0; k < KMAX; ++k) { w[j][k] = 0.0; nb[j][k] = 0; }
+    if (s < S) {
+      p0[j] = a.p0[(size_t)b * S + s];
+#pragma unroll
+      for (int k = 0; k < KMAX; ++k)
+        if (k < K) { w[j][k] = wb[(size_t)k * S + s]; nb[j][k] = col_src(m, b, s, k); }
+    }
+  }
+  for (int s = tid; s < S; s += nt) bufA[s] = 0.0;
+  if (tid < 3) slot[tid] = 0ull;
+  __syncthreads();
+
+  long long it = 0;
+  int r3 = 0;
+  double delta = 0.0;
+  for (;;) {
+    const double* din = (it & 1) ? bufB : bufA;
+    double* dout = (it & 1) ? bufA : bufB;
+    unsigned long long mx = 0ull;
+#pragma unroll
+    for (int j = 0; j < SPT; ++j) {
+      const int s = tid + j * nt;
+      if (s < S) {
+        double acc = 0.0;
+#pragma unroll
+        for (int k = 0; k < KMAX; ++k)
+          if (k < K) acc = fma(w[j][k], din[nb[j][k]], acc);
+        const double nv = p0[j] + acc;
+        dout[s] = nv;
+        const unsigned long long d = abs_bits(nv - cur[j]);
+        mx = d > mx ? d : mx;
+        cur[j] = nv;
+      }
+    }
+    mx = wave_max_u64(mx);
+    if ((tid & (kWave - 1)) == 0 && mx) atomicMax(&slot[r3], mx);
+    if (tid == 0) slot[r3 == 2 ? 0 : r3 + 1] = 0ull;
+    __syncthreads();
+    delta = bits_double(slot[r3]);
+    r3 = r3 == 2 ? 0 : r3 + 1;
+    ++it;
+    if (!(delta > a.eps)) break;
+    if (a.max_iter > 0 && it >= a.max_iter) break;
+  }
+#pragma unroll
+  for (int j = 0; j < SPT; ++j) {
+    const int s = tid + j * nt;
+    if (s < S) a.out[(size_t)b * S + s] = cur[j];
+  }
+  if (tid == 0) { a.iters[b] = it; a.status[b] = finish_status(delta, a.eps); }
+}
+
+struct BwdArgs {
+  Model m;
+  const double* w;  // [B'][K][S] collapsed weights
+  const double* reward;
+  const uint8_t* term;
+  int rescale;
+  double* pi;  // [B][S][A]
+  int32_t* status;
+};
+
+template <int SPT, int KMAX>
+__global__ void __launch_bounds__(1024) bwd_fused_kernel(BwdArgs a) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  const Model& m = a.m;
+  const int S = m.S, K = m.K, A = m.A;
+  const int b = blockIdx.x, tid = threadIdx.x, nt = blockDim.x;
+  double* bufA = (double*)smem;
+  double* bufB = bufA + S;
+  unsigned long long* slot = (unsigned long long*)(bufB + S);
+
+  double w[SPT][KMAX];
+  int nb[SPT][KMAX];
+  double er[SPT];
+  const double* wb = a.w + inst_of(m, b) * K * S;
+#pragma unroll
+  for (int j = 0; j < SPT; ++j) {
+    const int s = tid + j * nt;
+    er[j] = 0.0;
+#pragma unroll
+    for (int k = 0; k < KMAX; ++k) { w[j][k] = 0.0; nb[j][k] = 0; }
+    if (s < S) {
+      er[j] = exp(a.reward[(size_t)b * S + s]);
+#pragma unroll
+      for (int k = 0; k < KMAX; ++k)
+        if (k < K) { w[j][k] = wb[(size_t)k * S + s]; nb[j][k] = row_nbr(m, b, s, k); }
+    }
+  }
+  for (int s = tid; s < S; s += nt) bufA[s] = a.term[(size_t)b * S + s] ? 1.0 : 0.0;
+  if (tid < 3) slot[tid] = 0ull;
+  __syncthreads();
+
+  // 2*S sweeps in all (maxent.py:154): the first 2*S - 1 on the action-summed
+  // table, the last one per action because it also produces za.
+  const long long collapsed = 2LL * S - 1;
+  int e = 0, r3 = 0;
+  for (long long it = 0; it < collapsed; ++it) {
+    const double* din = (it & 1) ? bufB : bufA;
+    double* dout = (it & 1) ? bufA : bufB;
+    if (a.rescale && it > 0) e = rescale_exponent(bits_double(slot[r3 == 0 ? 2 : r3 - 1]));
+    unsigned long long mx = 0ull;
+#pragma unroll
+    for (int j = 0; j < SPT; ++j) {
+      const int s = tid + j * nt;
+      if (s < S) {
+        double acc = 0.0;
+#pragma unroll
+        for (int k = 0; k < KMAX; ++k)
+          if (k < K) acc = fma(w[j][k], din[nb[j][k]], acc);
+        const double nv = ldexp(er[j] * acc, e);
+        dout[s] = nv;
+        const unsigned long long d = abs_bits(nv);
+        mx = d > mx ? d : mx;
+      }
+    }
+    if (a.rescale) {
+      mx = wave_max_u64(mx);
+      if ((tid & (kWave - 1)) == 0 && mx) atomicMax(&slot[r3], mx);
+      if (tid == 0) slot[r3 == 2 ? 0 : r3 + 1] = 0ull;
+    }
+    __syncthreads();
+    r3 = r3 == 2 ? 0 : r3 + 1;
+  }
+  const double* zs = (collapsed & 1) ? bufB : bufA;
+  if (a.rescale && collapsed > 0) e = rescale_exponent(bits_double(slot[r3 == 0 ? 2 : r3 - 1]));
+#pragma unroll
+  for (int j = 0; j < SPT; ++j) {
+    const int s = tid + j * nt;
+    if (s < S) {
+      double za[kMaxActions];
+      double zsum = 0.0;
+      for (int act = 0; act < A; ++act) {
+        double acc = 0.0;
+#pragma unroll
+        for (int k = 0; k < KMAX; ++k)
+          if (k < K) acc = fma(row_val(m, b, act, k, s), zs[nb[j][k]], acc);
+        za[act] = ldexp(er[j] * acc, e);
+        zsum += za[act];
+      }
+      for (int act = 0; act < A; ++act) a.pi[((size_t)b * S + s) * A + act] = za[act] / zsum;
+    }
+  }
+  if (tid == 0) a.status[b] = IRLMX_OK;
+}
+
+struct SoftArgs {
+  Model m;
+  const double* reward;
+  const double* phi;  // soft: terminal reward; unused by VI
+  double discount;
+  double eps;
+  long long max_iter;
+  int average;  // VI only
+  double* pi;   // soft only, [B][S][A]
+  double* value;
+  int64_t* iters;
+  int32_t* status;
+};
+
+// per-state Bellman update shared by the fused and the sweep shapes.
+// NB: neighbour lookup; CACHED uses the per-thread register copy.
+template <bool SOFT, int KMAX, bool CACHED>
+__device__ inline double bellman_update(const SoftArgs& a, int b, int s, const int* nb,
+                                        const double* vin, double r, double phi) {
+  const Model& m = a.m;
+  const int K = m.K, A = m.A;
+  double v = SOFT ? phi : 0.0;
+#pragma unroll 1
+  for (int act = 0; act < A; ++act) {
+    double dot = 0.0;
+    if (CACHED) {
+#pragma unroll
+      for (int k = 0; k < KMAX; ++k)
+        if (k < K) dot = fma(row_val(m, b, act, k, s), vin[nb[k]], dot);
+    } else {
+      for (int k = 0; k < K; ++k) dot = fma(row_val(m, b, act, k, s), vin[row_nbr(m, b, s, k)], dot);
+    }
+    if (SOFT) {
+      v = softmax2(v, r + a.discount * dot);  // maxent.py:329-333
+    } else {
+      const double q = a.discount * dot;      // solver.py:44
+      if (a.average) v = act == 0 ? q : v + q;
+      else v = act == 0 ? q : ((v != v || q <= v) ? v : q);
+    }
+  }
+  if (!SOFT) v = r + (a.average ? v / (double)A : v);  // solver.py:47 / :99
+  return v;
+}
+
+template <int KMAX, bool CACHED>
+__device__ inline void soft_policy_row(const SoftArgs& a, int b, int s, const int* nb,
+                                       const double* vold, double vnew, double r) {
+  const Model& m = a.m;
+#pragma unroll 1
+  for (int act = 0; act < m.A; ++act) {
+    double dot = 0.0;
+    if (CACHED) {
+#pragma unroll
+      for (int k = 0; k < KMAX; ++k)
+        if (k < m.K) dot = fma(row_val(m, b, act, k, s), vold[nb[k]], dot);
+    } else {
+      for (int k = 0; k < m.K; ++k) dot = fma(row_val(m, b, act, k, s), vold[row_nbr(m, b, s, k)], dot);
+    }
+    const double q = r + a.discount * dot;
+    a.pi[((size_t)b * m.S + s) * m.A + act] = exp(q - vnew);  // maxent.py:341
+  }
+}
+
+template <bool SOFT, int SPT, int KMAX>
+__device__ __forceinline__ void bellman_fused_body(const SoftArgs& a, unsigned char* smem) {
+  const Model& m = a.m;
+  const int S = m.S, K = m.K;
+  const int b = blockIdx.x, tid = threadIdx.x, nt = blockDim.x;
+  double* bufA = (double*)smem;
+  double* bufB = bufA + S;
+  unsigned long long* slot = (unsigned long long*)(bufB + S);
+
+  int nb[SPT][KMAX];
+  double r[SPT], phi[SPT], cur[SPT];
+  const double v0 = SOFT ? -1e200 : 0.0;  // maxent.py:323 / solver.py:32
+#pragma unroll
+  for (int j = 0; j < SPT; ++j) {
+    const int s = tid + j * nt;
+    r[j] = 0.0;
+    phi[j] = 0.0;
+    cur[j] = v0;
+#pragma unroll
+    for (int k = 0; k < KMAX; ++k) nb[j][k] = 0;
+    if (s < S) {
+      r[j] = a.reward[(size_t)b * S + s];
+      if (SOFT) phi[j] = a.phi[(size_t)b * S + s];
+#pragma unroll
+      for (int k = 0; k < KMAX; ++k)
+        if (k < K) nb[j][k] = row_nbr(m, b, s, k);
+    }
+  }
+  for (int s = tid; s < S; s += nt) bufA[s] = v0;
+  if (tid < 3) slot[tid] = 0ull;
+  __syncthreads();
+
+  long long it = 0;
+  int r3 = 0;
+  double delta = 0.0;
+  for (;;) {
+    const double* vin = (it & 1) ? bufB : bufA;
+    double* vout = (it & 1) ? bufA : bufB;
+    unsigned long long mx = 0ull;
+#pragma unroll
+    for (int j = 0; j < SPT; ++j) {
+      const int s = tid + j * nt;
+      if (s < S) {
+        const double v = bellman_update<SOFT, KMAX, true>(a, b, s, nb[j], vin, r[j], phi[j]);
+        vout[s] = v;
+        const unsigned long long d = abs_bits(v - cur[j]);
+        mx = d > mx ? d : mx;
+        cur[j] = v;
+      }
+    }
+    mx = wave_max_u64(mx);
+    if ((tid & (kWave - 1)) == 0 && mx) atomicMax(&slot[r3], mx);
+    if (tid == 0) slot[r3 == 2 ? 0 : r3 + 1] = 0ull;
+    __syncthreads();
+    delta = bits_double(slot[r3]);
+    r3 = r3 == 2 ? 0 : r3 + 1;
+    ++it;
+    if (!(delta > a.eps)) break;
+    if (a.max_iter > 0 && it >= a.max_iter) break;
+  }
+  const double* vold = (it & 1) ? bufA : bufB;  // input of the last sweep
+#pragma unroll
+  for (int j = 0; j < SPT; ++j) {
+    const int s = tid + j * nt;
+    if (s < S) {
+      if (a.value) a.value[(size_t)b * S + s] = cur[j];
+      if (SOFT) soft_policy_row<KMAX, true>(a, b, s, nb[j], vold, cur[j], r[j]);
+    }
+  }
+  if (tid == 0) {
+    if (a.iters) a.iters[b] = it;
+    a.status[b] = finish_status(delta, a.eps);
+  }
+}
+
+template <int SPT, int KMAX>
+__global__ void __launch_bounds__(1024) soft_fused_kernel(SoftArgs a) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  bellman_fused_body<true, SPT, KMAX>(a, smem);
+}
+
+template <int SPT, int KMAX>
+__global__ void __launch_bounds__(1024) vi_fused_kernel(SoftArgs a) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  bellman_fused_body<false, SPT, KMAX>(a, smem);
+}
+
+// ---------------------------------------------------------------------------
+// sweep (one launch per sweep, all instances) kernels
+// ---------------------------------------------------------------------------
+
+__device__ inline void block_max_to(unsigned long long v, unsigned long long* dst) {
+  __shared__ unsigned long long red[kSweepThreads / kWave];
+  v = wave_max_u64(v);
+  const int wv = threadIdx.x / kWave;
+  if ((threadIdx.x & (kWave - 1)) == 0) red[wv] = v;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    unsigned long long m = 0;
+    for (int i = 0; i < (int)(blockDim.x / kWave); ++i) m = red[i] > m ? red[i] : m;
+    if (m) atomicMax(dst, m);
+  }
+}
+
+// Common prologue: decides whether instance b converged after the previous
+// sweep (`it` sweeps done so far); the first workgroup records the outcome.
+__device__ inline bool sweep_should_stop(int b, long long it, int r3, double eps, long long max_iter,
+                                         const Ws& ws, int32_t* status) {
+  if (ws.done[b]) return true;
+  if (it == 0) return false;
+  const double prev = bits_double(ws.slots[b * 3 + (r3 == 0 ? 2 : r3 - 1)]);
+  const bool cap = max_iter > 0 && it >= max_iter;
+  if (prev > eps && !cap) return false;
+  if (blockIdx.x == 0 && threadIdx.x == 0) {
+    ws.done[b] = 1;
+    ws.iters[b] = it;
+    status[b] = finish_status(prev, eps);
+    atomicAdd(ws.ndone, 1);
+  }
+  return true;
+}
+
+__global__ void __launch_bounds__(kSweepThreads)
+fwd_sweep_kernel(FwdArgs a, Ws ws, long long it, int r3) {
+  const Model& m = a.m;
+  const int b = blockIdx.y;
+  if (ws.bad[b]) {
+    if (blockIdx.x == 0 && threadIdx.x == 0 && !ws.done[b]) {
+      ws.done[b] = 1; ws.iters[b] = 1; a.status[b] = IRLMX_NONFINITE; atomicAdd(ws.ndone, 1);
+    }
+    return;
+  }
+  if (sweep_should_stop(b, it, r3, a.eps, a.max_iter, ws, a.status)) return;
+  const int S = m.S;
+  const int s = blockIdx.x * blockDim.x + threadIdx.x;
+  const double* din = ((it & 1) ? ws.buf1 : ws.buf0) + (size_t)b * S;
+  double* dout = ((it & 1) ? ws.buf0 : ws.buf1) + (size_t)b * S;
+  unsigned long long d = 0ull;
+  if (s < S) {
+    const double* wb = a.w + (size_t)b * m.Kc * S;
+    double acc = 0.0;
+    for (int k = 0; k < m.Kc; ++k) acc = fma(wb[(size_t)k * S + s], din[col_src(m, b, s, k)], acc);
+    const double nv = a.p0[(size_t)b * S + s] + acc;
+    dout[s] = nv;
+    d = abs_bits(nv - din[s]);
+  }
+  block_max_to(d, &ws.slots[b * 3 + r3]);
+  if (blockIdx.x == 0 && threadIdx.x == 0) ws.slots[b * 3 + (r3 == 2 ? 0 : r3 + 1)] = 0ull;
+}
+
+__global__ void fwd_finish_kernel(FwdArgs a, Ws ws) {
+  const int s = blockIdx.x * blockDim.x + threadIdx.x;
+  const int b = blockIdx.y;
+  const int S = a.m.S;
+  if (s >= S) return;
+  double v;
+  if (ws.bad[b]) v = __longlong_as_double(0x7ff8000000000000LL);
+  else v = ((ws.iters[b] & 1) ? ws.buf1 : ws.buf0)[(size_t)b * S + s];
+  a.out[(size_t)b * S + s] = v;
+  if (s == 0) a.iters[b] = ws.iters[b];
+}
+
+__global__ void __launch_bounds__(kSweepThreads)
+bwd_sweep_kernel(BwdArgs a, Ws ws, long long it, int r3) {
+  const Model& m = a.m;
+  const int S = m.S;
+  const int b = blockIdx.y;
+  const int s = blockIdx.x * blockDim.x + threadIdx.x;
+  const double* din = ((it & 1) ? ws.buf1 : ws.buf0) + (size_t)b * S;
+  double* dout = ((it & 1) ? ws.buf0 : ws.buf1) + (size_t)b * S;
+  int e = 0;
+  if (a.rescale && it > 0) e = rescale_exponent(bits_double(ws.slots[b * 3 + (r3 == 0 ? 2 : r3 - 1)]));
+  unsigned long long d = 0ull;
+  if (s < S) {
+    const double* wb = a.w + inst_of(m, b) * m.K * S;
+    double acc = 0.0;
+    for (int k = 0; k < m.K; ++k) acc = fma(wb[(size_t)k * S + s], din[row_nbr(m, b, s, k)], acc);
+    const double nv = ldexp(exp(a.reward[(size_t)b * S + s]) * acc, e);
+    dout[s] = nv;
+    d = abs_bits(nv);
+  }
+  if (a.rescale) {
+    block_max_to(d, &ws.slots[b * 3 + r3]);
+    if (blockIdx.x == 0 && threadIdx.x == 0) ws.slots[b * 3 + (r3 == 2 ? 0 : r3 + 1)] = 0ull;
+  }
+}
+
+__global__ void bwd_init_kernel(BwdArgs a, Ws ws) {
+  const int s = blockIdx.x * blockDim.x + threadIdx.x;
+  const int b = blockIdx.y;
+  if (s >= a.m.S) return;
+  ws.buf0[(size_t)b * a.m.S + s] = a.term[(size_t)b * a.m.S + s] ? 1.0 : 0.0;
+}
+
+__global__ void bwd_final_kernel(BwdArgs a, Ws ws, long long collapsed, int r3) {
+  const Model& m = a.m;
+  const int S = m.S, A = m.A;
+  const int b = blockIdx.y;
+  const int s = blockIdx.x * blockDim.x + threadIdx.x;
+  if (s >= S) return;
+  const double* zs = ((collapsed & 1) ? ws.buf1 : ws.buf0) + (size_t)b * S;
+  int e = 0;
+  if (a.rescale && collapsed > 0) e = rescale_exponent(bits_double(ws.slots[b * 3 + (r3 == 0 ? 2 : r3 - 1)]));
+  const double er = exp(a.reward[(size_t)b * S + s]);
+  double za[kMaxActions];
+  double zsum = 0.0;
+  for (int act = 0; act < A; ++act) {
+    double acc = 0.0;
+    for (int k = 0; k < m.K; ++k) acc = fma(row_val(m, b, act, k, s), zs[row_nbr(m, b, s, k)], acc);
+    za[act] = ldexp(er * acc, e);
+    zsum += za[act];
+  }
+  for (int act = 0; act < A; ++act) a.pi[((size_t)b * S + s) * A + act] = za[act] / zsum;
+  if (s == 0) a.status[b] = IRLMX_OK;
+}
+
+template <bool SOFT>
+__global__ void __launch_bounds__(kSweepThreads)
+bellman_sweep_kernel(SoftArgs a, Ws ws, long long it, int r3) {
+  const Model& m = a.m;
+  const int b = blockIdx.y;
+  if (sweep_should_stop(b, it, r3, a.eps, a.max_iter, ws, a.status)) return;
+  const int S = m.S;
+  const int s = blockIdx.x * blockDim.x + threadIdx.x;
+  const double* vin = ((it & 1) ? ws.buf1 : ws.buf0) + (size_t)b * S;
+  double* vout = ((it & 1) ? ws.buf0 : ws.buf1) + (size_t)b * S;
+  unsigned long long d = 0ull;
+  if (s < S) {
+    const double r = a.reward[(size_t)b * S + s];
+    const double phi = SOFT ? a.phi[(size_t)b * S + s] : 0.0;
+    const double v = bellman_update<SOFT, 1, false>(a, b, s, nullptr, vin, r, phi);
+    vout[s] = v;
+    d = abs_bits(v - vin[s]);
+  }
+  block_max_to(d, &ws.slots[b * 3 + r3]);
+  if (blockIdx.x == 0 && threadIdx.x == 0) ws.slots[b * 3 + (r3 == 2 ? 0 : r3 + 1)] = 0ull;
+}
+
+template <bool SOFT>
+__global__ void bellman_finish_kernel(SoftArgs a, Ws ws) {
+  const Model& m = a.m;
+  const int S = m.S;
+  const int b = blockIdx.y;
+  const int s = blockIdx.x * blockDim.x + threadIdx.x;
+  if (s >= S) return;
+  const long long it = ws.iters[b];
+  const double* vnew = ((it & 1) ? ws.buf1 : ws.buf0) + (size_t)b * S;
+  const double* vold = ((it & 1) ? ws.buf0 : ws.buf1) + (size_t)b * S;
+  if (a.value) a.value[(size_t)b * S + s] = vnew[s];
+  if (SOFT) soft_policy_row<1, false>(a, b, s, nullptr, vold, vnew[s], a.reward[(size_t)b * S + s]);
+  if (s == 0 && a.iters) a.iters[b] = it;
+}
+
+__global__ void fill_kernel(double* p, size_t n, double v) {
+  const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) p[i] = v;
+}
+
+// ---------------------------------------------------------------------------
+// host-side dispatch
+// ---------------------------------------------------------------------------
+
+struct FusedShape {
+  int spt;
+  int kmax;
+  int threads;
+};
+
+static int pick_kmax(int K) {
+  if (K <= 5) return 5;
+  if (K <= 8) return 8;
+  if (K <= 16) return 16;
+  if (K <= 32) return 32;
+  return 0;
+}
+
+// (SPT, KMAX) pairs instantiated per op: every pair listed compiles without
+// VGPR spills at __launch_bounds__(1024) (tools/kernel_resources.py); the soft
+// pass carries fp64 exp/log inline and so keeps fewer states per thread.
+static constexpr bool fused_pair_ok(int op, int spt, int kmax) {
+  switch (op) {
+    case IRLMX_OP_FORWARD:
+    case IRLMX_OP_BACKWARD:
+      return (kmax == 5 && spt <= 4) || (kmax == 8 && spt <= 2) || (kmax == 16 && spt <= 2) ||
+             (kmax == 32 && spt == 1);
+    case IRLMX_OP_SOFT_BACKWARD:
+      return (kmax == 5 && spt <= 2) || (kmax == 8 && spt == 1) || (kmax == 16 && spt == 1);
+    case IRLMX_OP_VALUE_ITERATION:
+      return (kmax == 5 && spt <= 4) || (kmax == 8 && spt <= 4) || (kmax == 16 && spt == 1) ||
+             (kmax == 32 && spt == 1);
+  }
+  return false;
+}
+
+static bool fused_shape(const Model& m, int op, FusedShape* out) {
+  if (m.S > fused_max_states() || m.A > kMaxActions) return false;
+  const int K = op == IRLMX_OP_FORWARD ? m.Kc : m.K;
+  const int kmax = pick_kmax(K);
+  if (!kmax) return false;
+  int spt = 1;
+  while ((m.S + spt - 1) / spt > 1024) spt *= 2;
+  if (!fused_pair_ok(op, spt, kmax)) return false;
+  const int per = (m.S + spt - 1) / spt;
+  out->spt = spt;
+  out->kmax = kmax;
+  out->threads = std::min(1024, ((per + kWave - 1) / kWave) * kWave);
+  return true;
+}
+
+static bool use_fused(const Model& m, int op) {
+  FusedShape f;
+  return fused_shape(m, op, &f);
+}
+
+static size_t fused_lds(const Model& m) { return 2 * (size_t)m.S * sizeof(double) + 4 * sizeof(unsigned long long); }
+
+// Kernel-pointer getters: only the (SPT, KMAX) pairs fused_pair_ok() admits
+// are instantiated.
+#define IRLMX_FUSED_GETTER(NAME, KERNEL_T, OP, ARGS_T)                    \
+  template <int S_, int K_>                                               \
+  static void (*NAME())(ARGS_T) {                                         \
+    if constexpr (fused_pair_ok(OP, S_, K_)) return &KERNEL_T<S_, K_>;    \
+    else return nullptr;                                                  \
+  }
+IRLMX_FUSED_GETTER(fwd_fused_ptr, fwd_fused_kernel, IRLMX_OP_FORWARD, FwdArgs)
+IRLMX_FUSED_GETTER(bwd_fused_ptr, bwd_fused_kernel, IRLMX_OP_BACKWARD, BwdArgs)
+IRLMX_FUSED_GETTER(soft_fused_ptr, soft_fused_kernel, IRLMX_OP_SOFT_BACKWARD, SoftArgs)
+IRLMX_FUSED_GETTER(vi_fused_ptr, vi_fused_kernel, IRLMX_OP_VALUE_ITERATION, SoftArgs)
+
+#define IRLMX_DISPATCH_FUSED(GETTER, SHAPE, B, LDS, STREAM, ARGS)                                   \
+  do {                                                                                                \
+    void (*kfn)(decltype(ARGS)) = nullptr;                                                           \
+    const int _s = (SHAPE).spt, _k = (SHAPE).kmax;                                                    \
+    if (_s == 1 && _k == 5) kfn = GETTER<1, 5>();                                                     \
+    else if (_s == 2 && _k == 5) kfn = GETTER<2, 5>();                                                \
+    else if (_s == 4 && _k == 5) kfn = GETTER<4, 5>();                                                \
+    else if (_s == 1 && _k == 8) kfn = GETTER<1, 8>();                                                \
+    else if (_s == 2 && _k == 8) kfn = GETTER<2, 8>();                                                \
+    else if (_s == 4 && _k == 8) kfn = GETTER<4, 8>();                                                \
+    else if (_s == 1 && _k == 16) kfn = GETTER<1, 16>();                                              \
+    else if (_s == 2 && _k == 16) kfn = GETTER<2, 16>();                                              \
+    else if (_s == 1 && _k == 32) kfn = GETTER<1, 32>();                                              \
+    if (!kfn) { set_error("no fused kernel for spt=%d kmax=%d", _s, _k); return IRLMX_EINVAL; }       \
+    hipError_t _e = hipFuncSetAttribute((const void*)kfn, hipFuncAttributeMaxDynamicSharedMemorySize, \
+                                        (int)(LDS));                                                  \
+    if (_e != hipSuccess) return hip_fail(_e, "hipFuncSetAttribute");                                \
+    hipLaunchKernelGGL(kfn, dim3(B), dim3((SHAPE).threads), (LDS), (STREAM), ARGS);                   \
+    _e = hipGetLastError();                                                                           \
+    if (_e != hipSuccess) return hip_fail(_e, #GETTER);                                               \
+  } while (0)
+
+static int validate(const irlmx_mdp* mdp) {
+  if (!mdp) { set_error("mdp is NULL"); return IRLMX_EINVAL; }
+  const Model m = make_model(mdp);
+  if (m.S <= 0 || m.A <= 0 || m.B <= 0) { set_error("bad sizes S=%d A=%d B=%d", m.S, m.A, m.B); return IRLMX_EINVAL; }
+  if (m.A > kMaxActions) { set_error("n_actions=%d exceeds %d", m.A, kMaxActions); return IRLMX_EINVAL; }
+  if (!m.row_val) { set_error("row_val is NULL"); return IRLMX_EINVAL; }
+  if (m.stencil) {
+    if ((long long)m.W * m.H != m.S) { set_error("stencil grid %dx%d != %d states", m.W, m.H, m.S); return IRLMX_EINVAL; }
+  } else if (mdp->layout == IRLMX_LAYOUT_ELL) {
+    if (!m.row_idx || m.K <= 0) { set_error("ELL row form missing"); return IRLMX_EINVAL; }
+  } else {
+    set_error("unknown layout %d", mdp->layout);
+    return IRLMX_EINVAL;
+  }
+  return 0;
+}
+
+static int check_ws(const Model& m, int op, size_t bytes, void* ws) {
+  const size_t need = carve(m, op, nullptr).total;
+  if (bytes < need || (need && !ws)) {
+    set_error("workspace too small: need %zu bytes, got %zu", need, bytes);
+    return IRLMX_EWORKSPACE;
+  }
+  return 0;
+}
+
+// Host poll loop of the sweep shape: enqueue `chunk` sweeps, read the done
+// counter, repeat.  Converged instances skip their sweeps, so over-enqueueing
+// costs only empty launches.
+template <typename LaunchOne>
+static int run_until_done(const Ws& ws, int B, hipStream_t st, LaunchOne&& one) {
+  long long it = 0;
+  int r3 = 0;
+  long long chunk = 32;
+  for (;;) {
+    for (long long c = 0; c < chunk; ++c) {
+      one(it, r3);
+      ++it;
+      r3 = r3 == 2 ? 0 : r3 + 1;
+    }
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return hip_fail(e, "sweep launch");
+    int32_t nd = 0;
+    e = hipMemcpyAsync(&nd, ws.ndone, sizeof(int32_t), hipMemcpyDeviceToHost, st);
+    if (e == hipSuccess) e = hipStreamSynchronize(st);
+    if (e != hipSuccess) return hip_fail(e, "poll");
+    if (nd >= B) return 0;
+    if (chunk < 4096) chunk *= 2;
+  }
+}
+
+}  // namespace irlmx
+
+using namespace irlmx;
+
+extern "C" size_t irlmx_workspace_bytes(const irlmx_mdp* mdp, int32_t op) {
+  if (validate(mdp)) return 0;
+  return carve(make_model(mdp), op, nullptr).total;
+}
+
+extern "C" int irlmx_forward_svf(const irlmx_mdp* mdp, const double* p_initial, const uint8_t* terminal,
+                                 const double* p_action, double eps, int64_t max_iter, double* svf,
+                                 int64_t* iterations, int32_t* status, void* workspace,
+                                 size_t workspace_bytes, void* stream) {
+  if (int rc = validate(mdp)) return rc;
+  const Model m = make_model(mdp);
+  if (!m.stencil && (!m.col_idx || !m.col_val || m.Kc <= 0)) { set_error("ELL column form missing"); return IRLMX_EINVAL; }
+  if (int rc = check_ws(m, IRLMX_OP_FORWARD, workspace_bytes, workspace)) return rc;
+  hipStream_t st = (hipStream_t)stream;
+  Ws ws = carve(m, IRLMX_OP_FORWARD, workspace);
+  hipError_t e = hipMemsetAsync(workspace, 0, ws.total, st);
+  if (e != hipSuccess) return hip_fail(e, "workspace memset");
+  const dim3 g((m.S + 255) / 256, m.B);
+  hipLaunchKernelGGL(fwd_weights_kernel, g, dim3(256), 0, st, m, p_action, terminal, ws.wgt, ws.bad);
+  FwdArgs a{m, ws.wgt, ws.bad, p_initial, eps, (long long)max_iter, svf, iterations, status};
+  FusedShape fs;
+  if (fused_shape(m, IRLMX_OP_FORWARD, &fs)) {
+    IRLMX_DISPATCH_FUSED(fwd_fused_ptr, fs, m.B, fused_lds(m), st, a);
+    return 0;
+  }
+  const dim3 gs((m.S + kSweepThreads - 1) / kSweepThreads, m.B);
+  int rc = run_until_done(ws, m.B, st, [&](long long it, int r3) {
+    hipLaunchKernelGGL(fwd_sweep_kernel, gs, dim3(kSweepThreads), 0, st, a, ws, it, r3);
+  });
+  if (rc) return rc;
+  hipLaunchKernelGGL(fwd_finish_kernel, g, dim3(256), 0, st, a, ws);
+  e = hipGetLastError();
+  return e == hipSuccess ? 0 : hip_fail(e, "fwd_finish");
+}
+
+extern "C" int irlmx_backward_maxent(const irlmx_mdp* mdp, const double* reward, const uint8_t* terminal,
+                                     int32_t rescale, double* p_action, int32_t* status, void* workspace,
+                                     size_t workspace_bytes, void* stream) {
+  if (int rc = validate(mdp)) return rc;
+  const Model m = make_model(mdp);
+  if (int rc = check_ws(m, IRLMX_OP_BACKWARD, workspace_bytes, workspace)) return rc;
+  hipStream_t st = (hipStream_t)stream;
+  Ws ws = carve(m, IRLMX_OP_BACKWARD, workspace);
+  hipError_t e = hipMemsetAsync(workspace, 0, ws.total, st);
+  if (e != hipSuccess) return hip_fail(e, "workspace memset");
+  hipLaunchKernelGGL(bwd_weights_kernel, dim3((m.S + 255) / 256, m.shared ? 1 : m.B), dim3(256), 0, st, m, ws.wgt);
+  BwdArgs a{m, ws.wgt, reward, terminal, rescale, p_action, status};
+  FusedShape fs;
+  if (fused_shape(m, IRLMX_OP_BACKWARD, &fs)) {
+    IRLMX_DISPATCH_FUSED(bwd_fused_ptr, fs, m.B, fused_lds(m), st, a);
+    return 0;
+  }
+  const dim3 g((m.S + kSweepThreads - 1) / kSweepThreads, m.B);
+  hipLaunchKernelGGL(bwd_init_kernel, g, dim3(kSweepThreads), 0, st, a, ws);
+  const long long collapsed = 2LL * m.S - 1;
+  int r3 = 0;
+  for (long long it = 0; it < collapsed; ++it) {
+    hipLaunchKernelGGL(bwd_sweep_kernel, g, dim3(kSweepThreads), 0, st, a, ws, it, r3);
+    r3 = r3 == 2 ? 0 : r3 + 1;
+  }
+  hipLaunchKernelGGL(bwd_final_kernel, g, dim3(kSweepThreads), 0, st, a, ws, collapsed, r3);
+  e = hipGetLastError();
+  return e == hipSuccess ? 0 : hip_fail(e, "backward");
+}
+
+static int bellman_common(const irlmx_mdp* mdp, const double* reward, const double* phi, double discount,
+                          double eps, int64_t max_iter, int average, double* p_action, double* value,
+                          int64_t* iterations, int32_t* status, void* workspace, size_t workspace_bytes,
+                          void* stream, bool soft) {
+  if (int rc = validate(mdp)) return rc;
+  const Model m = make_model(mdp);
+  const int op = soft ? IRLMX_OP_SOFT_BACKWARD : IRLMX_OP_VALUE_ITERATION;
+  if (int rc = check_ws(m, op, workspace_bytes, workspace)) return rc;
+  hipStream_t st = (hipStream_t)stream;
+  Ws ws = carve(m, op, workspace);
+  hipError_t e = hipMemsetAsync(workspace, 0, ws.total, st);
+  if (e != hipSuccess) return hip_fail(e, "workspace memset");
+  SoftArgs a{m, reward, phi, discount, eps, (long long)max_iter, average, p_action, value, iterations, status};
+  FusedShape fs;
+  if (fused_shape(m, op, &fs)) {
+    if (soft) IRLMX_DISPATCH_FUSED(soft_fused_ptr, fs, m.B, fused_lds(m), st, a);
+    else IRLMX_DISPATCH_FUSED(vi_fused_ptr, fs, m.B, fused_lds(m), st, a);
+    return 0;
+  }
+  const dim3 g((m.S + kSweepThreads - 1) / kSweepThreads, m.B);
+  const size_t n = (size_t)m.B * m.S;
+  hipLaunchKernelGGL(fill_kernel, dim3((n + 255) / 256), dim3(256), 0, st, ws.buf0, n, soft ? -1e200 : 0.0);
+  int rc = run_until_done(ws, m.B, st, [&](long long it, int r3) {
+    if (soft) hipLaunchKernelGGL(bellman_sweep_kernel<true>, g, dim3(kSweepThreads), 0, st, a, ws, it, r3);
+    else hipLaunchKernelGGL(bellman_sweep_kernel<false>, g, dim3(kSweepThreads), 0, st, a, ws, it, r3);
+  });
+  if (rc) return rc;
+  if (soft) hipLaunchKernelGGL(bellman_finish_kernel<true>, g, dim3(kSweepThreads), 0, st, a, ws);
+  else hipLaunchKernelGGL(bellman_finish_kernel<false>, g, dim3(kSweepThreads), 0, st, a, ws);
+  e = hipGetLastError();
+  return e == hipSuccess ? 0 : hip_fail(e, "bellman finish");
+}
+
+extern "C" int irlmx_soft_backward(const irlmx_mdp* mdp, const double* reward, const double* terminal_reward,
+                                   double discount, double eps, int64_t max_iter, double* p_action,
+                                   double* value, int64_t* iterations, int32_t* status, void* workspace,
+                                   size_t workspace_bytes, void* stream) {
+  return bellman_common(mdp, reward, terminal_reward, discount, eps, max_iter, 0, p_action, value, iterations,
+                        status, workspace, workspace_bytes, stream, true);
+}
+
+extern "C" int irlmx_value_iteration(const irlmx_mdp* mdp, const double* reward, double discount, double eps,
+                                     int32_t average, int64_t max_iter, double* value, int64_t* iterations,
+                                     int32_t* status, void* workspace, size_t workspace_bytes, void* stream) {
+  return bellman_common(mdp, reward, nullptr, discount, eps, max_iter, average, nullptr, value, iterations,
+                        status, workspace, workspace_bytes, stream, false);
+}

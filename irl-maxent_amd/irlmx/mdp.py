@@ -1,0 +1,203 @@
+"""Transition models resident in HBM.
+
+The reference hands the solvers a dense float64 ``p_transition[from, to,
+action]`` (gridworld.py:124-142) and re-slices it per call (maxent.py:98-102,
+143, 320; solver.py:37).  ``DeviceMDP`` holds the same model once, compactly:
+
+* ``STENCIL5`` -- every nonzero of P lies on the 5-point stencil of a
+  width x height grid (all reference gridworlds).  ``row_val[b][a][k][s]`` is
+  ``P[s, nbr_k(s), a]`` for k = self, +x, -x, +y, -y: 5*A float64 per state
+  (160 B at A = 4) instead of S*A*8 B per state dense.
+* ``ELL`` -- any other sparsity: per state the union of targets over actions
+  (row form, ``row_idx``/``row_val``) and, for the forward pass, the union of
+  sources (column form, ``col_idx``/``col_val``).
+
+Instances: a model holds B tables, or one table shared by B instances
+(``shared=True``), e.g. one world with B reward vectors.
+"""
+
+import ctypes
+import math
+
+import numpy as np
+import torch
+
+from . import _lib
+
+
+def _is_square(n):
+    r = math.isqrt(n)
+    return r if r * r == n else 0
+
+
+class DeviceMDP:
+    def __init__(self, layout, n_states, n_actions, batch, shared, row_val, row_idx=None,
+                 col_idx=None, col_val=None, width=0, height=0, k_row=5, k_col=5, device=None):
+        self.layout = layout
+        self.n_states = int(n_states)
+        self.n_actions = int(n_actions)
+        self.batch = int(batch)
+        self.shared = bool(shared)
+        self.row_val = row_val
+        self.row_idx = row_idx
+        self.col_idx = col_idx
+        self.col_val = col_val
+        self.width = int(width)
+        self.height = int(height)
+        self.k_row = int(k_row)
+        self.k_col = int(k_col)
+        self.device = device if device is not None else row_val.device
+        self._struct = None
+
+    # -- construction ------------------------------------------------------
+
+    @classmethod
+    def icy_gridworld(cls, size, p_slip=0.2, device=None):
+        """IcyGridWorld(size, p_slip) tables built on the device (gridworld.py:177-248).
+
+        ``p_slip`` may be a sequence: one table per value (batch = len(p_slip)).
+        """
+        device = _lib.require_device(device)
+        lib = _lib.load()
+        slips = np.atleast_1d(np.asarray(p_slip, dtype=np.float64))
+        B, S = len(slips), size * size
+        d_slip = torch.as_tensor(slips, device=device)
+        row_val = torch.empty((B, 4, 5, S), dtype=torch.float64, device=device)
+        _lib.check(lib.irlmx_build_icy_gridworld(size, _lib.ptr(d_slip), B, _lib.ptr(row_val),
+                                                 _lib.stream_ptr(device)), "build_icy_gridworld")
+        return cls(_lib.LAYOUT_STENCIL5, S, 4, B, False, row_val, width=size, height=size, device=device)
+
+    @classmethod
+    def gridworld(cls, size, batch=1, device=None):
+        """Deterministic GridWorld(size) tables (gridworld.py:23-171)."""
+        device = _lib.require_device(device)
+        lib = _lib.load()
+        S = size * size
+        row_val = torch.empty((batch, 4, 5, S), dtype=torch.float64, device=device)
+        _lib.check(lib.irlmx_build_gridworld(size, batch, _lib.ptr(row_val), _lib.stream_ptr(device)),
+                   "build_gridworld")
+        return cls(_lib.LAYOUT_STENCIL5, S, 4, batch, False, row_val, width=size, height=size, device=device)
+
+    @classmethod
+    def from_dense(cls, p_transition, device=None, grid=None):
+        """Upload a dense ``[S, S, A]`` table (one instance, shared layout).
+
+        The STENCIL5 layout is used when every nonzero lies on the stencil of a
+        square (or ``grid=(width, height)``) grid; otherwise ELL.
+        """
+        device = _lib.require_device(device)
+        lib = _lib.load()
+        p = np.asarray(p_transition)
+        if p.ndim != 3 or p.shape[0] != p.shape[1]:
+            raise ValueError(f"p_transition must have shape (S, S, A), got {p.shape}")
+        S, _, A = p.shape
+        p = np.ascontiguousarray(p, dtype=np.float64)
+        if grid is not None:
+            w, h = grid
+        else:
+            w = h = _is_square(S)
+        if w and w * h == S:
+            dense = torch.from_numpy(p).to(device)
+            row_val = torch.empty((1, A, 5, S), dtype=torch.float64, device=device)
+            flag = torch.zeros(1, dtype=torch.int32, device=device)
+            _lib.check(lib.irlmx_dense_to_stencil(_lib.ptr(dense), w, h, A, _lib.ptr(row_val), _lib.ptr(flag),
+                                                  _lib.stream_ptr(device)), "dense_to_stencil")
+            off = int(flag.item())
+            del dense
+            if not off:
+                return cls(_lib.LAYOUT_STENCIL5, S, A, 1, True, row_val, width=w, height=h, device=device)
+        return cls._ell_from_dense(p, device)
+
+    @classmethod
+    def _ell_from_dense(cls, p, device):
+        S, _, A = p.shape
+        nz = p != 0.0
+        any_a = nz.any(axis=2)                      # [s, t]
+        # row form: union of targets per source state, ascending
+        k_row = max(1, int(any_a.sum(axis=1).max()))
+        row_idx = np.tile(np.arange(S, dtype=np.int32), (k_row, 1))  # pad: self, value 0
+        row_val = np.zeros((A, k_row, S))
+        src, tgt = np.nonzero(any_a)
+        slot = _slots(src, S)
+        row_idx[slot, src] = tgt
+        row_val[:, slot, src] = p[src, tgt, :].T
+        # column form: union of sources per target state, ascending
+        tgt2, src2 = np.nonzero(any_a.T)
+        k_col = max(1, int(any_a.sum(axis=0).max()))
+        col_idx = np.tile(np.arange(S, dtype=np.int32), (k_col, 1))
+        col_val = np.zeros((A, k_col, S))
+        slot2 = _slots(tgt2, S)
+        col_idx[slot2, tgt2] = src2
+        col_val[:, slot2, tgt2] = p[src2, tgt2, :].T
+        t = lambda a, dt: torch.from_numpy(np.ascontiguousarray(a)).to(device=device, dtype=dt)[None]
+        return cls(_lib.LAYOUT_ELL, S, A, 1, True, t(row_val, torch.float64), row_idx=t(row_idx, torch.int32),
+                   col_idx=t(col_idx, torch.int32), col_val=t(col_val, torch.float64), k_row=k_row,
+                   k_col=k_col, device=device)
+
+    # -- views -------------------------------------------------------------
+
+    def with_batch(self, batch):
+        """The same single table applied to ``batch`` instances (shared)."""
+        if not self.shared and self.batch != 1:
+            raise ValueError("with_batch needs a single-table model")
+        return DeviceMDP(self.layout, self.n_states, self.n_actions, batch, True, self.row_val, self.row_idx,
+                         self.col_idx, self.col_val, self.width, self.height, self.k_row, self.k_col,
+                         self.device)
+
+    def select(self, lo, hi):
+        """Instances [lo, hi) of a batched (non-shared) model, as a view."""
+        if self.shared:
+            return self.with_batch(hi - lo)
+        sl = lambda t: t[lo:hi] if t is not None else None
+        return DeviceMDP(self.layout, self.n_states, self.n_actions, hi - lo, False, sl(self.row_val),
+                         sl(self.row_idx), sl(self.col_idx), sl(self.col_val), self.width, self.height,
+                         self.k_row, self.k_col, self.device)
+
+    def struct(self):
+        """The ``irlmx_mdp`` C struct (pointers stay valid while self is alive)."""
+        if self._struct is None:
+            s = _lib.MDPStruct()
+            s.layout = self.layout
+            s.n_states = self.n_states
+            s.n_actions = self.n_actions
+            s.width = self.width
+            s.height = self.height
+            s.k_row = self.k_row if self.layout == _lib.LAYOUT_ELL else 5
+            s.k_col = self.k_col if self.layout == _lib.LAYOUT_ELL else 5
+            s.batch = self.batch
+            s.shared = 1 if self.shared else 0
+            s.row_val = self.row_val.data_ptr()
+            s.row_idx = self.row_idx.data_ptr() if self.row_idx is not None else 0
+            s.col_idx = self.col_idx.data_ptr() if self.col_idx is not None else 0
+            s.col_val = self.col_val.data_ptr() if self.col_val is not None else 0
+            self._struct = s
+        return ctypes.byref(self._struct)
+
+    def to_dense(self, b=0):
+        """Dense ``[S, S, A]`` numpy table of instance b (tests and small sizes only)."""
+        S, A = self.n_states, self.n_actions
+        out = np.zeros((S, S, A))
+        rv = self.row_val[0 if self.shared else b].cpu().numpy()
+        if self.layout == _lib.LAYOUT_STENCIL5:
+            s = np.arange(S)
+            x, y = s % self.width, s // self.width
+            nbrs = [s, np.where(x + 1 < self.width, s + 1, -1), np.where(x > 0, s - 1, -1),
+                    np.where(y + 1 < self.height, s + self.width, -1), np.where(y > 0, s - self.width, -1)]
+            for k, t in enumerate(nbrs):
+                ok = t >= 0
+                for a in range(A):
+                    out[s[ok], t[ok], a] = rv[a, k, ok]
+        else:
+            ri = self.row_idx[0 if self.shared else b].cpu().numpy()
+            for k in range(self.k_row):
+                for a in range(A):
+                    np.add.at(out, (np.arange(S), ri[k], a), rv[a, k])
+        return out
+
+
+def _slots(keys, n):
+    """Position of each entry among the entries with the same key (keys sorted)."""
+    if len(keys) == 0:
+        return np.zeros(0, dtype=np.int64)
+    starts = np.searchsorted(keys, np.arange(n))
+    return np.arange(len(keys)) - starts[keys]

@@ -1,0 +1,148 @@
+"""Batched device operations of the MaxEnt-IRL inner loop (torch tensors in/out).
+
+Every function runs on the HIP device through libirlmx.so; inputs are float64
+(or uint8 masks) of shape [B, ...] and stay resident in HBM.  These are the
+building blocks of the numpy drop-ins (``maxent``, ``solver``) and of the
+batched IRL driver (``irlmx.batch``).
+"""
+
+import numpy as np
+import torch
+
+from . import _lib
+from .mdp import DeviceMDP
+
+_workspaces = {}
+
+
+def _workspace(mdp, op):
+    lib = _lib.load()
+    n = int(lib.irlmx_workspace_bytes(mdp.struct(), op))
+    key = (mdp.device, op)
+    ws = _workspaces.get(key)
+    if ws is None or ws.numel() < n:
+        ws = torch.empty(max(n, 256), dtype=torch.uint8, device=mdp.device)
+        _workspaces[key] = ws
+    return ws, n
+
+
+def _f64(x, mdp, shape):
+    t = torch.as_tensor(x, dtype=torch.float64, device=mdp.device)
+    return t.reshape(shape).contiguous()
+
+
+def terminal_mask(terminal, n_states, batch=1, device=None):
+    """uint8 [B, S] mask with the reference's indexing semantics (maxent.py:99, 147).
+
+    ``terminal`` is indexed into a numpy vector exactly as the reference indexes
+    with it, so negative indices, duplicates and invalid index types behave (or
+    raise) the same way.
+    """
+    m = np.zeros(n_states, dtype=np.uint8)
+    m[terminal] = 1
+    return torch.as_tensor(np.tile(m, (batch, 1)), device=device)
+
+
+def backward_maxent(mdp, reward, terminal, rescale=True):
+    """Local action probabilities [B, S, A] (maxent.py:119-159)."""
+    lib = _lib.load()
+    B, S, A = mdp.batch, mdp.n_states, mdp.n_actions
+    r = _f64(reward, mdp, (B, S))
+    term = terminal.to(device=mdp.device, dtype=torch.uint8).reshape(B, S).contiguous()
+    pi = torch.empty((B, S, A), dtype=torch.float64, device=mdp.device)
+    status = torch.empty(B, dtype=torch.int32, device=mdp.device)
+    ws, n = _workspace(mdp, _lib.OP_BACKWARD)
+    _lib.check(lib.irlmx_backward_maxent(mdp.struct(), _lib.ptr(r), _lib.ptr(term), 1 if rescale else 0,
+                                         _lib.ptr(pi), _lib.ptr(status), _lib.ptr(ws), n,
+                                         _lib.stream_ptr(mdp.device)), "backward_maxent")
+    return pi
+
+
+def forward_svf(mdp, p_initial, terminal, p_action, eps=1e-5, max_iter=0):
+    """Expected state-visitation frequencies (maxent.py:63-114).
+
+    Returns ``(svf [B, S], iterations [B] int64, status [B] int32)``.
+    """
+    lib = _lib.load()
+    B, S, A = mdp.batch, mdp.n_states, mdp.n_actions
+    p0 = _f64(p_initial, mdp, (B, S))
+    pi = _f64(p_action, mdp, (B, S, A))
+    term = terminal.to(device=mdp.device, dtype=torch.uint8).reshape(B, S).contiguous()
+    svf = torch.empty((B, S), dtype=torch.float64, device=mdp.device)
+    iters = torch.empty(B, dtype=torch.int64, device=mdp.device)
+    status = torch.empty(B, dtype=torch.int32, device=mdp.device)
+    ws, n = _workspace(mdp, _lib.OP_FORWARD)
+    _lib.check(lib.irlmx_forward_svf(mdp.struct(), _lib.ptr(p0), _lib.ptr(term), _lib.ptr(pi), float(eps),
+                                     int(max_iter), _lib.ptr(svf), _lib.ptr(iters), _lib.ptr(status),
+                                     _lib.ptr(ws), n, _lib.stream_ptr(mdp.device)), "forward_svf")
+    return svf, iters, status
+
+
+def soft_backward(mdp, reward, terminal_reward, discount, eps=1e-5, max_iter=0):
+    """MaxCausalEnt soft value iteration (maxent.py:279-341).
+
+    Returns ``(p_action [B, S, A], value [B, S], iterations [B], status [B])``.
+    """
+    lib = _lib.load()
+    B, S, A = mdp.batch, mdp.n_states, mdp.n_actions
+    r = _f64(reward, mdp, (B, S))
+    phi = _f64(terminal_reward, mdp, (B, S))
+    pi = torch.empty((B, S, A), dtype=torch.float64, device=mdp.device)
+    v = torch.empty((B, S), dtype=torch.float64, device=mdp.device)
+    iters = torch.empty(B, dtype=torch.int64, device=mdp.device)
+    status = torch.empty(B, dtype=torch.int32, device=mdp.device)
+    ws, n = _workspace(mdp, _lib.OP_SOFT_BACKWARD)
+    _lib.check(lib.irlmx_soft_backward(mdp.struct(), _lib.ptr(r), _lib.ptr(phi), float(discount), float(eps),
+                                       int(max_iter), _lib.ptr(pi), _lib.ptr(v), _lib.ptr(iters),
+                                       _lib.ptr(status), _lib.ptr(ws), n, _lib.stream_ptr(mdp.device)),
+               "soft_backward")
+    return pi, v, iters, status
+
+
+def value_iteration(mdp, reward, discount, eps=1e-3, average=False, max_iter=0):
+    """Hard-max (solver.py:9-52) or action-average (solver.py:55-104) value iteration.
+
+    Returns ``(value [B, S], iterations [B], status [B])``.
+    """
+    lib = _lib.load()
+    B, S = mdp.batch, mdp.n_states
+    r = _f64(reward, mdp, (B, S))
+    v = torch.empty((B, S), dtype=torch.float64, device=mdp.device)
+    iters = torch.empty(B, dtype=torch.int64, device=mdp.device)
+    status = torch.empty(B, dtype=torch.int32, device=mdp.device)
+    ws, n = _workspace(mdp, _lib.OP_VALUE_ITERATION)
+    _lib.check(lib.irlmx_value_iteration(mdp.struct(), _lib.ptr(r), float(discount), float(eps),
+                                         1 if average else 0, int(max_iter), _lib.ptr(v), _lib.ptr(iters),
+                                         _lib.ptr(status), _lib.ptr(ws), n, _lib.stream_ptr(mdp.device)),
+               "value_iteration")
+    return v, iters, status
+
+
+def optimal_policy(successor, value):
+    """argmax_a value[successor[s, a]] per state, first index on ties (solver.py:107-124)."""
+    lib = _lib.load()
+    succ = successor.to(dtype=torch.int32).contiguous()
+    S, A = succ.shape
+    value = value.to(dtype=torch.float64).reshape(-1, S).contiguous()
+    B = value.shape[0]
+    out = torch.empty((B, S), dtype=torch.int64, device=value.device)
+    _lib.check(lib.irlmx_optimal_policy(_lib.ptr(succ), S, A, B, _lib.ptr(value), _lib.ptr(out),
+                                        _lib.stream_ptr(value.device)), "optimal_policy")
+    return out
+
+
+def stochastic_policy(successor, weighted_value):
+    """w(value)[successor] normalised per state (solver.py:155-181)."""
+    lib = _lib.load()
+    succ = successor.to(dtype=torch.int32).contiguous()
+    S, A = succ.shape
+    wv = weighted_value.to(dtype=torch.float64).reshape(-1, S).contiguous()
+    B = wv.shape[0]
+    out = torch.empty((B, S, A), dtype=torch.float64, device=wv.device)
+    _lib.check(lib.irlmx_stochastic_policy(_lib.ptr(succ), S, A, B, _lib.ptr(wv), _lib.ptr(out),
+                                           _lib.stream_ptr(wv.device)), "stochastic_policy")
+    return out
+
+
+__all__ = ["DeviceMDP", "terminal_mask", "backward_maxent", "forward_svf", "soft_backward",
+           "value_iteration", "optimal_policy", "stochastic_policy"]

@@ -1,0 +1,150 @@
+"""Pin the CPU oracle against golden vectors produced by the reference itself.
+
+The fixtures under tests/golden/ come from tools/gen_golden.py, which imports
+the reference (narendasan/irl-maxent, src/) read-only.  The oracle evaluates
+the same numpy statements in the same order, so these checks are bit-exact
+(``np.array_equal``) including the sweep counts of every fixed-point loop.
+"""
+
+import hashlib
+
+import numpy as np
+import pytest
+
+import maxent_oracle as O
+from conftest import load_golden, unpack_trajectories
+
+# forward passes longer than this are skipped on CPU (the oracle needs minutes)
+CPU_SWEEP_BUDGET = 200_000
+
+
+def _cases(z):
+    return [str(n) for n in z["names"]]
+
+
+def test_world_tables_bit_exact():
+    z = load_golden("worlds")
+    for size, p_slip in ((5, 0.2), (8, 0.1), (8, 0.3), (3, 0.2)):
+        assert np.array_equal(O.icy_gridworld_table(size, p_slip), z[f"icy_{size}_{p_slip}"])
+    assert np.array_equal(O.gridworld_table(5), z["det_5"])
+    h = hashlib.sha256(np.ascontiguousarray(O.icy_gridworld_table(16, 0.2)).tobytes()).hexdigest()
+    assert h == str(z["icy_16_0.2_sha256"])
+    h = hashlib.sha256(np.ascontiguousarray(O.gridworld_table(16)).tobytes()).hexdigest()
+    assert h == str(z["det_16_sha256"])
+
+
+def test_config1_pipeline_pieces():
+    z = load_golden("config1")
+    P = z["p_transition"]
+    assert np.array_equal(P, O.icy_gridworld_table(5, 0.2))
+    v, k = O.value_iteration(P, z["reward"], 0.7)
+    assert np.array_equal(v, z["value"]) and k == int(z["vi_sweeps"])
+    assert np.array_equal(O.optimal_policy_from_value(5, v), z["opt_policy"])
+    assert np.array_equal(O.stochastic_policy_from_value(5, v, w=lambda x: x ** 5), z["policy"])
+    tjs = unpack_trajectories(z["traj_flat"], z["traj_lens"])
+    feats = np.identity(25)
+    assert np.array_equal(O.feature_expectation(feats, tjs), z["e_features"])
+    assert np.array_equal(O.initial_probabilities(25, tjs), z["p_initial"])
+    term = [int(t) for t in z["terminal"]]
+    pi = O.backward_maxent(P, term, np.ones(25))
+    assert np.array_equal(pi, z["pi1"])
+    assert np.array_equal(O.backward_maxent(P, term, np.ones(25), rescale=True), z["pi1"])
+    svf, k = O.forward_svf(P, z["p_initial"], term, pi)
+    assert np.array_equal(svf, z["svf1"]) and k == int(z["k_f1"])
+    cpi, _, ks = O.soft_backward(P, term, np.ones(25), 0.7)
+    assert np.array_equal(cpi, z["cpi1"]) and ks == int(z["k_s1"])
+    csvf, k = O.forward_svf(P, z["p_initial"], term, cpi)
+    assert np.array_equal(csvf, z["csvf1"]) and k == int(z["k_cf1"])
+
+
+def test_config1_irl_full_run():
+    z = load_golden("config1")
+    P = z["p_transition"]
+    tjs = unpack_trajectories(z["traj_flat"], z["traj_lens"])
+    term = [int(t) for t in z["terminal"]]
+    r, steps = O.irl(P, np.identity(25), term, tjs, O.ExpSga(lr=O.linear_decay(0.2)), O.Constant(1.0))
+    assert steps == int(z["irl_steps"])
+    assert np.array_equal(r, z["reward_maxent"])
+
+
+@pytest.mark.slow
+def test_config1_irl_causal_full_run():
+    z = load_golden("config1")
+    P = z["p_transition"]
+    tjs = unpack_trajectories(z["traj_flat"], z["traj_lens"])
+    term = [int(t) for t in z["terminal"]]
+    r, steps = O.irl_causal(P, np.identity(25), term, tjs, O.ExpSga(lr=O.linear_decay(0.2)),
+                            O.Constant(1.0), 0.7)
+    assert steps == int(z["causal_steps"])
+    assert np.array_equal(r, z["reward_causal"])
+
+
+def test_maxent_small_cases():
+    z = load_golden("maxent_small")
+    for c in _cases(z):
+        P = O.icy_gridworld_table(int(z[c + "__size"]), float(z[c + "__p_slip"]))
+        term = [int(t) for t in z[c + "__terminal"]]
+        with np.errstate(all="ignore"):
+            pi = O.backward_maxent(P, term, z[c + "__reward"])
+        assert np.array_equal(pi, z[c + "__pi"], equal_nan=True), c
+        if np.isfinite(pi).all():
+            # power-of-two rescaling leaves the ratio bit-identical where finite
+            assert np.array_equal(O.backward_maxent(P, term, z[c + "__reward"], rescale=True), pi), c
+        if int(z[c + "__k_f"]) > CPU_SWEEP_BUDGET:
+            continue
+        with np.errstate(all="ignore"):
+            svf, k = O.forward_svf(P, z[c + "__p0"], term, pi)
+        assert np.array_equal(svf, z[c + "__svf"], equal_nan=True), c
+        assert k == int(z[c + "__k_f"]), c
+
+
+def test_value_iteration_cases():
+    z = load_golden("vi")
+    for c in _cases(z):
+        size = int(z[c + "__size"])
+        P = O.icy_gridworld_table(size, 0.2)
+        avg = bool(z[c + "__average"])
+        v, k = O.value_iteration(P, z[c + "__reward"], float(z[c + "__discount"]), average=avg)
+        assert np.array_equal(v, z[c + "__value"]) and k == int(z[c + "__k"]), c
+        if not avg:
+            assert np.array_equal(O.optimal_policy_from_value(size, v), z[c + "__opt_policy"])
+            sp = O.stochastic_policy_from_value(size, v, w=lambda x: np.exp(x))
+            assert np.array_equal(sp, z[c + "__stoch_policy"])
+    P = O.gridworld_table(4)
+    v, k = O.value_iteration(P, z["det4__reward"], 0.5)
+    assert np.array_equal(v, z["det4__value"]) and k == int(z["det4__k"])
+    assert np.array_equal(O.optimal_policy_from_value(4, v), z["det4__opt_policy"])
+
+
+def test_generic_mdps():
+    z = load_golden("generic")
+    for c in _cases(z):
+        P = z[c + "__P"]
+        term = [int(t) for t in z[c + "__terminal"]]
+        r, p0 = z[c + "__reward"], z[c + "__p0"]
+        pi = O.backward_maxent(P, term, r)
+        assert np.array_equal(pi, z[c + "__pi"]), c
+        svf, k = O.forward_svf(P, p0, term, pi)
+        assert np.array_equal(svf, z[c + "__svf"]) and k == int(z[c + "__k_f"]), c
+        cpi, _, ks = O.soft_backward(P, term, r, 0.8)
+        assert np.array_equal(cpi, z[c + "__cpi"]) and ks == int(z[c + "__k_s"]), c
+        v, kv = O.value_iteration(P, r, 0.9)
+        assert np.array_equal(v, z[c + "__v"]) and kv == int(z[c + "__k_v"]), c
+        va, kva = O.value_iteration(P, r, 0.9, average=True)
+        assert np.array_equal(va, z[c + "__va"]) and kva == int(z[c + "__k_va"]), c
+
+
+def test_causal_small_cases():
+    z = load_golden("causal_small")
+    for c in _cases(z):
+        size = int(z[c + "__size"])
+        P = O.icy_gridworld_table(size, 0.2)
+        term = [int(t) for t in z[c + "__terminal"]]
+        pi, _, ks = O.soft_backward(P, term, z[c + "__reward"], float(z[c + "__discount"]))
+        assert np.array_equal(pi, z[c + "__pi"]) and ks == int(z[c + "__k_s"]), c
+        if size <= 16:
+            svf, k = O.forward_svf(P, z[c + "__p0"], term, pi)
+            assert np.array_equal(svf, z[c + "__svf"]) and k == int(z[c + "__k_f"]), c
+    P = O.icy_gridworld_table(5, 0.2)
+    pi, _, ks = O.soft_backward(P, z["phi_vec__phi"], np.ones(25), 0.8)
+    assert np.array_equal(pi, z["phi_vec__pi"]) and ks == int(z["phi_vec__k_s"])
