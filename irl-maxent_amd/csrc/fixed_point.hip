@@ -32,6 +32,7 @@
 #include <cstring>
 #include <vector>
 
+#include "cluster.h"
 #include "common.h"
 
 namespace irlmx {
@@ -113,6 +114,12 @@ struct Ws {
   int32_t* done;              // [B]
   int64_t* iters;             // [B]
   int32_t* ndone;             // [1]
+  // cluster shape (stencil layouts too large for one CU)
+  double* pub;                // [2][B][S]
+  unsigned long long* cslots; // [B][3][kTMax]
+  unsigned int* counter;      // [B]
+  unsigned long long* growth; // [B]
+  int* err;                   // [1]
   size_t total;
 };
 
@@ -142,6 +149,12 @@ static Ws carve(const Model& m, int op, void* base) {
   w.done = (int32_t*)take(B * sizeof(int32_t));
   w.iters = (int64_t*)take(B * sizeof(int64_t));
   w.ndone = (int32_t*)take(sizeof(int32_t) * 4);
+  const bool cl = sweep && m.stencil && (op == IRLMX_OP_FORWARD || op == IRLMX_OP_BACKWARD);
+  w.pub = (double*)take(cl ? 2 * B * S * sizeof(double) : 0);
+  w.cslots = (unsigned long long*)take(cl ? B * 3 * kTMax * sizeof(unsigned long long) : 0);
+  w.counter = (unsigned int*)take(cl ? B * sizeof(unsigned int) : 0);
+  w.growth = (unsigned long long*)take(cl ? B * sizeof(unsigned long long) : 0);
+  w.err = (int*)take(cl ? 4 * sizeof(int) : 0);
   w.total = off;
   return w;
 }
@@ -359,7 +372,7 @@ __global__ void __launch_bounds__(1024) bwd_fused_kernel(BwdArgs a) {
 #pragma unroll
         for (int k = 0; k < KMAX; ++k)
           if (k < K) acc = fma(w[j][k], din[nb[j][k]], acc);
-        const double nv = ldexp(er[j] * acc, e);
+        const double nv = ldexp(__dmul_rn(er[j], acc), e);
         dout[s] = nv;
         const unsigned long long d = abs_bits(nv);
         mx = d > mx ? d : mx;
@@ -386,8 +399,8 @@ __global__ void __launch_bounds__(1024) bwd_fused_kernel(BwdArgs a) {
 #pragma unroll
         for (int k = 0; k < KMAX; ++k)
           if (k < K) acc = fma(row_val(m, b, act, k, s), zs[nb[j][k]], acc);
-        za[act] = ldexp(er[j] * acc, e);
-        zsum += za[act];
+        za[act] = ldexp(__dmul_rn(er[j], acc), e);  // rounded product, then the sum (maxent.py:155-156)
+        zsum = __dadd_rn(zsum, za[act]);
       }
       for (int act = 0; act < A; ++act) a.pi[((size_t)b * S + s) * A + act] = za[act] / zsum;
     }
@@ -428,14 +441,14 @@ __device__ inline double bellman_update(const SoftArgs& a, int b, int s, const i
       for (int k = 0; k < K; ++k) dot = fma(row_val(m, b, act, k, s), vin[row_nbr(m, b, s, k)], dot);
     }
     if (SOFT) {
-      v = softmax2(v, r + a.discount * dot);  // maxent.py:329-333
+      v = softmax2(v, __dadd_rn(r, __dmul_rn(a.discount, dot)));  // maxent.py:329-333
     } else {
-      const double q = a.discount * dot;      // solver.py:44
-      if (a.average) v = act == 0 ? q : v + q;
+      const double q = __dmul_rn(a.discount, dot);  // solver.py:44
+      if (a.average) v = act == 0 ? q : __dadd_rn(v, q);
       else v = act == 0 ? q : ((v != v || q <= v) ? v : q);
     }
   }
-  if (!SOFT) v = r + (a.average ? v / (double)A : v);  // solver.py:47 / :99
+  if (!SOFT) v = __dadd_rn(r, a.average ? v / (double)A : v);  // solver.py:47 / :99
   return v;
 }
 
@@ -453,7 +466,7 @@ __device__ inline void soft_policy_row(const SoftArgs& a, int b, int s, const in
     } else {
       for (int k = 0; k < m.K; ++k) dot = fma(row_val(m, b, act, k, s), vold[row_nbr(m, b, s, k)], dot);
     }
-    const double q = r + a.discount * dot;
+    const double q = __dadd_rn(r, __dmul_rn(a.discount, dot));
     a.pi[((size_t)b * m.S + s) * m.A + act] = exp(q - vnew);  // maxent.py:341
   }
 }
@@ -635,7 +648,7 @@ bwd_sweep_kernel(BwdArgs a, Ws ws, long long it, int r3) {
     const double* wb = a.w + inst_of(m, b) * m.K * S;
     double acc = 0.0;
     for (int k = 0; k < m.K; ++k) acc = fma(wb[(size_t)k * S + s], din[row_nbr(m, b, s, k)], acc);
-    const double nv = ldexp(exp(a.reward[(size_t)b * S + s]) * acc, e);
+    const double nv = ldexp(__dmul_rn(exp(a.reward[(size_t)b * S + s]), acc), e);
     dout[s] = nv;
     d = abs_bits(nv);
   }
@@ -667,8 +680,8 @@ __global__ void bwd_final_kernel(BwdArgs a, Ws ws, long long collapsed, int r3) 
   for (int act = 0; act < A; ++act) {
     double acc = 0.0;
     for (int k = 0; k < m.K; ++k) acc = fma(row_val(m, b, act, k, s), zs[row_nbr(m, b, s, k)], acc);
-    za[act] = ldexp(er * acc, e);
-    zsum += za[act];
+    za[act] = ldexp(__dmul_rn(er, acc), e);
+    zsum = __dadd_rn(zsum, za[act]);
   }
   for (int act = 0; act < A; ++act) a.pi[((size_t)b * S + s) * A + act] = za[act] / zsum;
   if (s == 0) a.status[b] = IRLMX_OK;
@@ -889,6 +902,16 @@ extern "C" int irlmx_forward_svf(const irlmx_mdp* mdp, const double* p_initial, 
     IRLMX_DISPATCH_FUSED(fwd_fused_ptr, fs, m.B, fused_lds(m), st, a);
     return 0;
   }
+  ClusterPlan cp;
+  if (m.stencil && cluster_plan(m.W, m.H, m.B, &cp)) {
+    ClusterArgs ca{};
+    ca.W = m.W; ca.H = m.H; ca.S = m.S; ca.A = m.A;
+    ca.wgt = ws.wgt; ca.vin = p_initial; ca.bad = ws.bad;
+    ca.eps = eps; ca.max_iter = (long long)max_iter;
+    ca.pub = ws.pub; ca.slots = ws.cslots; ca.counter = ws.counter; ca.err = ws.err;
+    ca.out = svf; ca.iters = iterations; ca.status = status;
+    return cluster_run(kModeFwd, cp, ca, m.B, st);
+  }
   const dim3 gs((m.S + kSweepThreads - 1) / kSweepThreads, m.B);
   int rc = run_until_done(ws, m.B, st, [&](long long it, int r3) {
     hipLaunchKernelGGL(fwd_sweep_kernel, gs, dim3(kSweepThreads), 0, st, a, ws, it, r3);
@@ -915,6 +938,19 @@ extern "C" int irlmx_backward_maxent(const irlmx_mdp* mdp, const double* reward,
   if (fused_shape(m, IRLMX_OP_BACKWARD, &fs)) {
     IRLMX_DISPATCH_FUSED(bwd_fused_ptr, fs, m.B, fused_lds(m), st, a);
     return 0;
+  }
+  ClusterPlan cp;
+  if (m.stencil && m.A <= kMaxActions && cluster_plan(m.W, m.H, m.B, &cp)) {
+    hipLaunchKernelGGL(bwd_growth_kernel, dim3(m.B), dim3(1024), 0, st, ws.wgt, m.shared ? 1 : 0, reward, m.S,
+                       ws.growth);
+    ClusterArgs ca{};
+    ca.W = m.W; ca.H = m.H; ca.S = m.S; ca.A = m.A;
+    ca.tab_shared = m.shared ? 1 : 0;
+    ca.wgt = ws.wgt; ca.row_val = m.row_val; ca.vin = reward; ca.term = terminal; ca.growth = ws.growth;
+    ca.n_sweeps = 2LL * m.S - 1; ca.rescale = rescale;
+    ca.pub = ws.pub; ca.slots = ws.cslots; ca.counter = ws.counter; ca.err = ws.err;
+    ca.out = p_action; ca.status = status;
+    return cluster_run(kModeBwd, cp, ca, m.B, st);
   }
   const dim3 g((m.S + kSweepThreads - 1) / kSweepThreads, m.B);
   hipLaunchKernelGGL(bwd_init_kernel, g, dim3(kSweepThreads), 0, st, a, ws);

@@ -49,13 +49,25 @@ def dev():
     return irlmx.require_device()
 
 
-@pytest.fixture(params=["fused", "sweep"])
+@pytest.fixture(params=["fused", "sweep", "cluster"])
 def shape(request, monkeypatch):
-    """Run each case through both execution shapes of the kernels."""
+    """Run each case through every execution shape of the kernels.
+
+    fused   : one workgroup per instance (the default below 4096 states)
+    sweep   : one launch per sweep over all instances
+    cluster : persistent tiles of 3 rows with 2 ghost rows (forced small so the
+              golden cases exercise the halo exchange, the in-block rollback of
+              the forward pass and the block-boundary rescaling of the backward)
+    """
+    for k in ("IRLMX_FUSED_MAX_STATES", "IRLMX_CLUSTER", "IRLMX_CLUSTER_R", "IRLMX_CLUSTER_G"):
+        monkeypatch.delenv(k, raising=False)
     if request.param == "sweep":
         monkeypatch.setenv("IRLMX_FUSED_MAX_STATES", "0")
-    else:
-        monkeypatch.delenv("IRLMX_FUSED_MAX_STATES", raising=False)
+        monkeypatch.setenv("IRLMX_CLUSTER", "0")
+    elif request.param == "cluster":
+        monkeypatch.setenv("IRLMX_FUSED_MAX_STATES", "0")
+        monkeypatch.setenv("IRLMX_CLUSTER_R", "3")
+        monkeypatch.setenv("IRLMX_CLUSTER_G", "2")
     return request.param
 
 
@@ -157,7 +169,7 @@ def test_maxent_small_cases(dev, shape):
         tm = ops.terminal_mask(term, n, device=dev)
         ref_pi = z[c + "__pi"]
         if shape == "sweep" and int(z[c + "__k_f"]) > 100_000:
-            continue  # millions of one-sweep launches; the fused shape covers this case
+            continue  # millions of one-sweep launches; the fused and cluster shapes cover it
         if np.isfinite(ref_pi).all():
             pi = ops.backward_maxent(mdp, z[c + "__reward"], tm)
             close(pi[0].cpu().numpy(), ref_pi, what=c + " pi")
@@ -290,3 +302,35 @@ def test_max_iter_cap(dev):
         O.icy_gridworld_table(5, 0.2), [24], np.ones(25)), max_iter=10)
     assert int(k[0]) == 10 == kr and int(st[0]) == 2
     close(svf[0].cpu().numpy(), ref, what="capped svf")
+
+
+def test_shapes_bit_identical(dev, monkeypatch):
+    """fused, sweep and cluster shapes run the same float64 operations in the same
+    order (no implicit FMA contraction, power-of-two rescaling only), so their
+    policies, SVFs and sweep counts agree bit for bit -- including the cluster's
+    halo exchange, in-block rollback and block-boundary rescaling."""
+    from irlmx import DeviceMDP, ops
+    shapes = {"fused": {}, "sweep": {"IRLMX_FUSED_MAX_STATES": "0", "IRLMX_CLUSTER": "0"},
+              "cluster": {"IRLMX_FUSED_MAX_STATES": "0", "IRLMX_CLUSTER_R": "3", "IRLMX_CLUSTER_G": "2"},
+              "cluster1": {"IRLMX_FUSED_MAX_STATES": "0", "IRLMX_CLUSTER_R": "5", "IRLMX_CLUSTER_G": "4"}}
+    rng = np.random.default_rng(3)
+    for size, theta, cap in ((8, "ones", 0), (9, "unif", 20000), (12, "ones", 0)):
+        n = size * size
+        r = np.ones(n) if theta == "ones" else rng.uniform(0, 1.5, n)
+        p0 = np.zeros(n)
+        p0[0] = 1.0
+        mdp = DeviceMDP.icy_gridworld(size, 0.2, device=dev)
+        tm = ops.terminal_mask([n - 1], n, device=dev)
+        out = {}
+        for name, env in shapes.items():
+            for k in ("IRLMX_FUSED_MAX_STATES", "IRLMX_CLUSTER", "IRLMX_CLUSTER_R", "IRLMX_CLUSTER_G"):
+                monkeypatch.delenv(k, raising=False)
+            for k, v in env.items():
+                monkeypatch.setenv(k, v)
+            pi = ops.backward_maxent(mdp, r, tm)
+            svf, k, _ = ops.forward_svf(mdp, p0, tm, pi, max_iter=cap)
+            out[name] = (pi, svf, int(k[0]))
+        for name in ("sweep", "cluster", "cluster1"):
+            assert torch.equal(out["fused"][0], out[name][0]), (size, name, "pi")
+            assert torch.equal(out["fused"][1], out[name][1]), (size, name, "svf")
+            assert out["fused"][2] == out[name][2], (size, name)

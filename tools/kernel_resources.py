@@ -9,7 +9,7 @@ import sys
 
 def main(files):
     for f in files:
-        out = subprocess.run(["hipcc", "-O3", "-std=c++17", "--offload-arch=gfx950", "-c", "-o", "/dev/null", f,
+        out = subprocess.run(["hipcc", "-O3", "-std=c++17", "--offload-arch=gfx950", "-ffp-contract=off", "-c", "-o", "/dev/null", f,
                               "-Rpass-analysis=kernel-resource-usage"], capture_output=True, text=True).stderr
         cur = None
         rows = {}
