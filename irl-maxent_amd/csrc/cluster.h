@@ -33,6 +33,7 @@ struct ClusterArgs {
   unsigned long long* slots;  // [B][3][kTMax]
   unsigned int* counter;   // [B]
   int* err;                // [1] barrier timeout
+  unsigned long long* stamps;  // optional [grid][8] phase cycle counters (IRLMX_STAMPS=1), else null
   double* out;             // forward: svf [B][S]; backward: pi [B][S][A]
   int64_t* iters;
   int32_t* status;

@@ -40,6 +40,7 @@
 
 #include <algorithm>
 #include <cmath>
+#include <cstdio>
 #include <cstdlib>
 
 #include "cluster.h"
@@ -50,35 +51,54 @@ namespace irlmx {
 void set_error(const char* fmt, ...);
 int hip_fail(hipError_t e, const char* what);
 
-__device__ inline unsigned int ld_acq_relaxed(unsigned int* p) {
+__device__ inline unsigned int ld_sc1(unsigned int* p) {
   return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
+__device__ inline void st_sc1(double* p, double v) {  // write-through (sc1) 8-byte store
+  __hip_atomic_store((unsigned long long*)p, (unsigned long long)__double_as_longlong(v), __ATOMIC_RELAXED,
+                     __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ inline double ld_sc1(const double* p) {  // L1-bypassing (sc1) 8-byte load
+  return __longlong_as_double((long long)__hip_atomic_load((unsigned long long*)p, __ATOMIC_RELAXED,
+                                                           __HIP_MEMORY_SCOPE_AGENT));
+}
 
-// Arrival barrier of the C tiles of one instance (see file comment).  Returns
-// false on timeout (then the error word is set and the caller exits).
+// Arrival barrier of the C tiles of one instance, in the fence-free form of
+// MI355X_MICROARCH.md "Valid forms" (row 1): every payload byte is stored
+// write-through (sc1) and loaded with sc1 loads, every storing wave drains
+// (s_waitcnt vmcnt(0)) before the workgroup barrier, then ONE lane adds to the
+// instance's arrival counter (agent scope) and polls it with sc1 loads; the
+// other waves load after the workgroup barrier that lane joins.  Bounded by a
+// 20 s wall-clock timeout; returns false on timeout (error word set).
 __device__ inline bool instance_barrier(unsigned int* counter, unsigned int target, int* err, int* lds_flag) {
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every storing wave drains its stores
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
   if (threadIdx.x == 0) {
     int abort = 0;
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __hip_atomic_fetch_add(counter, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();  // 100 MHz
-    while (ld_acq_relaxed(counter) < target) {
+    while (ld_sc1(counter) < target) {
       __builtin_amdgcn_s_sleep(1);
-      if (__builtin_amdgcn_s_memrealtime() - t0 > 2000000000ull) {  // 20 s
+      if (__builtin_amdgcn_s_memrealtime() - t0 > 2000000000ull) {
         abort = 1;
         atomicOr(err, 1);
         break;
       }
     }
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     *lds_flag = abort;
   }
   __syncthreads();
   return *lds_flag == 0;
+}
+
+__device__ inline unsigned long long stamp_now() { return __builtin_amdgcn_s_memtime(); }
+
+// OR of a 32-bit value over the wave (one ballot per bit that may be set).
+__device__ inline unsigned wave_or_bits(unsigned v, int nbits) {
+  unsigned out = 0;
+  for (int b = 0; b < nbits; ++b)
+    if (__ballot((v >> b) & 1u)) out |= 1u << b;
+  return out;
 }
 
 // LDS buffer layout: [W + 1 zeros][E states][W + 1 zeros].  With the pads, the
@@ -86,6 +106,13 @@ __device__ inline bool instance_barrier(unsigned int* counter, unsigned int targ
 // q = buf + l + 1: one address register per state and constant offsets (the
 // pads are never written and stay 0; their stencil weight is 0 or the row they
 // feed is a ghost row that is no longer exact).
+//
+// Per-sweep convergence bookkeeping (forward): the reference stops after the
+// first sweep whose max|d_new - d_old| is not > eps, NaN included.  So per
+// sweep i of a block two facts suffice: "some |delta| > eps" (bit i) and "some
+// |delta| is NaN" (bit 16 + i).  Threads collect them in a register, and the
+// tile ORs them once per block (ballots, one LDS atomic per wave, one global
+// atomic per tile) -- no per-sweep reduction.
 template <int MODE, int SPT, int WT>
 __global__ void __launch_bounds__(kCT) cluster_kernel(ClusterArgs a) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
@@ -98,13 +125,16 @@ __global__ void __launch_bounds__(kCT) cluster_kernel(ClusterArgs a) {
   const int e0 = max(0, r0 - a.G), e1 = min(H, r1 + a.G);
   const int E = (e1 - e0) * W;
   const int own0 = (r0 - e0) * W, own1 = (r1 - e0) * W;
+  // owned rows other tiles read as ghosts: within G rows of either tile edge
+  const int pubA1 = min(own1, own0 + a.G * W), pubB0 = max(pubA1, own1 - a.G * W);
   const int base = e0 * W;
   const int pad = W + 1;
   const int blen = a.emax + 2 * pad;
   double* bufA = (double*)smem;
   double* bufB = bufA + blen;
-  unsigned long long* red = (unsigned long long*)(bufB + blen);  // [2][kTMax]
-  int* lflag = (int*)(red + 2 * kTMax);                          // [4]
+  double* snap = bufB + blen;                                            // forward: block-start state
+  unsigned long long* red = (unsigned long long*)(snap + (MODE == kModeFwd ? a.emax : 0));  // [2]
+  int* lflag = (int*)(red + 2);                                          // [4]
 
   const size_t iS = (size_t)inst * S;
   if (MODE == kModeFwd && a.bad[inst]) {
@@ -130,6 +160,11 @@ __global__ void __launch_bounds__(kCT) cluster_kernel(ClusterArgs a) {
 #pragma unroll
       for (int k = 0; k < kStencilK; ++k) w[j][k] = a.wgt[wbase + (size_t)k * S + s];
     }
+    // pin the constants in registers: without this the compiler re-loads them
+    // from global memory inside every sweep (rematerialisation of invariant loads)
+#pragma unroll
+    for (int k = 0; k < kStencilK; ++k) asm volatile("" : "+v"(w[j][k]));
+    asm volatile("" : "+v"(c0[j]));
   }
   for (int i = tid; i < 2 * blen; i += kCT) bufA[i] = 0.0;
   __syncthreads();
@@ -138,8 +173,9 @@ __global__ void __launch_bounds__(kCT) cluster_kernel(ClusterArgs a) {
     if (MODE == kModeBwd) v0 = a.term[iS + base + l] ? 1.0 : 0.0;
     bufA[pad + l] = v0;
     bufB[pad + l] = v0;
+    if (MODE == kModeFwd) snap[l] = v0;
   }
-  if (tid < 2 * kTMax) red[tid] = 0ull;
+  if (tid < 2) red[tid] = 0ull;
   if (tid == 0) lflag[0] = 0;
 
   int T = a.T;
@@ -153,88 +189,128 @@ __global__ void __launch_bounds__(kCT) cluster_kernel(ClusterArgs a) {
   }
   __syncthreads();
 
-  // one Jacobi sweep over the extended tile; the owned-row maximum goes to *rslot
-  auto sweep = [&](const double* din, double* dout, unsigned long long* rslot) {
+  const double eps = a.eps;
+  // One Jacobi sweep over the extended tile.  Forward: sets bit i / 16 + i of
+  // `flags` for an owned |delta| > eps / NaN.  Backward: when `want_max`,
+  // returns this thread's max over owned states (for the block-end rescale).
+  // Every slot l < SPT * kCT is swept, also l >= E: those have zero weights and
+  // zero c0, read only zeros (buffers are zero-filled and hold emax + 2 pads),
+  // and stay 0 -- which is what state E - 1's down-neighbour must read.  No
+  // per-state branch, so all LDS reads of a sweep can be in flight together.
+  auto sweep = [&](const double* __restrict__ din, double* __restrict__ dout, int i, unsigned& flags,
+                   bool want_max) {
     unsigned long long mx = 0ull;
 #pragma unroll
     for (int j = 0; j < SPT; ++j) {
       const int l = tid + j * kCT;
-      if (l < E) {
-        const double* q = din + l + 1;
-        const double self = q[W];
-        double acc = fma(w[j][0], self, 0.0);  // same association as the fused/sweep shapes
-        acc = fma(w[j][1], q[W + 1], acc);
-        acc = fma(w[j][2], q[W - 1], acc);
-        acc = fma(w[j][3], q[2 * W], acc);
-        acc = fma(w[j][4], q[0], acc);
-        const double nv = MODE == kModeFwd ? __dadd_rn(c0[j], acc) : __dmul_rn(c0[j], acc);
-        dout[pad + l] = nv;
-        if (l >= own0 && l < own1) {
-          const unsigned long long d = MODE == kModeFwd ? abs_bits(nv - self) : abs_bits(nv);
+      const double* q = din + l + 1;
+      const double self = q[W];
+      double acc = fma(w[j][0], self, 0.0);
+      acc = fma(w[j][1], q[W + 1], acc);
+      acc = fma(w[j][2], q[W - 1], acc);
+      acc = fma(w[j][3], q[2 * W], acc);
+      acc = fma(w[j][4], q[0], acc);
+      const double nv = MODE == kModeFwd ? c0[j] + acc : c0[j] * acc;
+      dout[pad + l] = nv;
+      if (l >= own0 && l < own1) {
+        if (MODE == kModeFwd) {
+          const double d = fabs(nv - self);
+          flags |= ((d > eps) ? 1u : 0u) << i;
+          flags |= ((d != d) ? 1u : 0u) << (16 + i);
+        } else if (want_max) {
+          const unsigned long long d = abs_bits(nv);
           mx = d > mx ? d : mx;
         }
       }
     }
-    mx = wave_max_u64(mx);
-    if ((tid & (kWave - 1)) == 0 && mx) atomicMax(rslot, mx);
     __syncthreads();
+    return mx;
   };
 
-  unsigned long long* slots = a.slots + (size_t)inst * 3 * kTMax;
+  unsigned int* slots = (unsigned int*)(a.slots + (size_t)inst * 3 * kTMax);  // [3] words (fwd masks / bwd max)
+  unsigned long long* slots64 = a.slots + (size_t)inst * 3 * kTMax;
   const size_t pubStride = (size_t)a.btot * S;  // pub[parity] stride
 
   double* cur = bufA;
   double* oth = bufB;
   long long done = 0;  // sweeps completed before the current block
+  // phase cycle counters (thread 0): sweeps, summary + publish, barrier, refresh, blocks
+  unsigned long long st_acc[5] = {0, 0, 0, 0, 0};
+  const bool stamps = a.stamps != nullptr && tid == 0;
+  unsigned long long ts = stamps ? stamp_now() : 0;
+  auto stamp = [&](int k) {
+    if (stamps) { const unsigned long long t = stamp_now(); st_acc[k] += t - ts; ts = t; }
+  };
+  auto stamp_flush = [&]() {
+    if (stamps) for (int k = 0; k < 5; ++k) a.stamps[(size_t)blockIdx.x * 8 + k] = st_acc[k];
+  };
   const long long total = MODE == kModeBwd ? a.n_sweeps : -1;
   for (int m = 0;; ++m) {
     int Tm = T;
     if (MODE == kModeBwd) Tm = (int)min<long long>((long long)T, total - done);
-    unsigned long long* rset = red + (m & 1) * kTMax;
     // ---- T_m sweeps on chip ----------------------------------------------
+    unsigned flags = 0;
+    unsigned long long mx = 0ull;
     for (int i = 0; i < Tm; ++i) {
-      sweep(cur, oth, &rset[i]);
+      mx = sweep(cur, oth, i, flags, i == Tm - 1);
       double* t = cur; cur = oth; oth = t;
     }
-    // ---- publish owned rows, combine per-sweep maxima, arrive --------------
+    stamp(0);
+    if (stamps) st_acc[4] += 1;
+    // ---- per-tile summary of the block -------------------------------------
+    if (MODE == kModeFwd) {
+      const unsigned wf = wave_or_bits(flags, 16 + Tm) & (((1u << Tm) - 1) | (((1u << Tm) - 1) << 16));
+      if ((tid & (kWave - 1)) == 0 && wf) atomicOr((unsigned*)&red[m & 1], wf);
+    } else if (a.rescale) {
+      mx = wave_max_u64(mx);
+      if ((tid & (kWave - 1)) == 0 && mx) atomicMax(&red[m & 1], mx);
+    }
+    // ---- publish halo rows (write-through), combine the summaries, arrive ----
     double* pubm = a.pub + (size_t)(m & 1) * pubStride + iS;
-    for (int l = own0 + tid; l < own1; l += kCT) pubm[base + l] = cur[pad + l];
+    for (int l = own0 + tid; l < pubA1; l += kCT) st_sc1(&pubm[base + l], cur[pad + l]);
+    for (int l = pubB0 + tid; l < own1; l += kCT) st_sc1(&pubm[base + l], cur[pad + l]);
+    __syncthreads();  // the tile summary in red[m & 1] is complete
     if (tid == 0) {
-      unsigned long long* sl = slots + (m % 3) * kTMax;
-      for (int i = 0; i < Tm; ++i)
-        if (rset[i]) atomicMax(&sl[i], rset[i]);
-      if (tile == 0) {
-        unsigned long long* nx = slots + ((m + 1) % 3) * kTMax;
-        for (int i = 0; i < kTMax; ++i) __hip_atomic_store(&nx[i], 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      const unsigned long long v = red[m & 1];
+      if (MODE == kModeFwd) {
+        if (v) atomicOr(&slots[m % 3], (unsigned)v);
+      } else if (v) {
+        atomicMax(&slots64[(m % 3) + 3], v);
+      }
+      if (tile == 0) {  // the ring entry of block m + 1 was last read before barrier m - 1
+        __hip_atomic_store(&slots[(m + 1) % 3], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(&slots64[((m + 1) % 3) + 3], 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       }
     }
+    stamp(1);
     if (!instance_barrier(&a.counter[inst], (unsigned)(a.C * (m + 1)), a.err, &lflag[0])) return;
-    // every tile now sees every tile's publication and maxima of block m;
-    // the other maxima set was last read before this barrier: clear it for block m + 1
-    if (tid < kTMax) red[((m + 1) & 1) * kTMax + tid] = 0ull;
-    unsigned long long* sl = slots + (m % 3) * kTMax;
+    stamp(2);
+    if (tid == 0) red[(m + 1) & 1] = 0ull;  // next block's summary word (last read above)
     if (MODE == kModeFwd) {
+      const unsigned msk = __hip_atomic_load(&slots[m % 3], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       int conv = 0;
-      double dl = 0.0;
+      bool nan_stop = false;
       for (int i = 0; i < Tm; ++i) {
-        dl = bits_double(__hip_atomic_load(&sl[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
         const bool cap = a.max_iter > 0 && done + i + 1 >= a.max_iter;
-        if (!(dl > a.eps) || cap) { conv = i + 1; break; }
+        nan_stop = (msk >> (16 + i)) & 1u;
+        if (nan_stop || !((msk >> i) & 1u) || cap) { conv = i + 1; break; }
       }
       if (conv) {
         // exact stop inside the block: replay `conv` sweeps from the block-start state
-        const double* src = m == 0 ? nullptr : a.pub + (size_t)((m - 1) & 1) * pubStride + iS;
-        for (int l = tid; l < E; l += kCT) cur[pad + l] = src ? src[base + l] : 0.0;
+        for (int l = tid; l < E; l += kCT) cur[pad + l] = snap[l];
         __syncthreads();
-        unsigned long long* scratch = red + ((m + 1) & 1) * kTMax;
+        unsigned scratch = 0;
         for (int i = 0; i < conv; ++i) {
-          sweep(cur, oth, scratch);
+          sweep(cur, oth, i, scratch, false);
           double* t = cur; cur = oth; oth = t;
         }
         for (int l = own0 + tid; l < own1; l += kCT) a.out[iS + base + l] = cur[pad + l];
+        stamp(3);
+        stamp_flush();
         if (tile == 0 && tid == 0) {
+          const bool big = (msk >> (conv - 1)) & 1u;
           a.iters[inst] = done + conv;
-          a.status[inst] = dl != dl ? IRLMX_NONFINITE : (dl > a.eps ? IRLMX_MAXITER : IRLMX_OK);
+          a.status[inst] = nan_stop ? IRLMX_NONFINITE : (big ? IRLMX_MAXITER : IRLMX_OK);
         }
         return;
       }
@@ -243,15 +319,19 @@ __global__ void __launch_bounds__(kCT) cluster_kernel(ClusterArgs a) {
     // ---- refresh ghost rows from the neighbours' publications ---------------
     int e_scale = 0;
     if (MODE == kModeBwd && a.rescale)
-      e_scale = rescale_exponent(bits_double(__hip_atomic_load(&sl[Tm - 1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)));
+      e_scale = rescale_exponent(bits_double(
+          __hip_atomic_load(&slots64[(m % 3) + 3], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)));
     for (int l = tid; l < E; l += kCT) {
-      double v = (l >= own0 && l < own1) ? cur[pad + l] : pubm[base + l];
+      double v = (l >= own0 && l < own1) ? cur[pad + l] : ld_sc1(&pubm[base + l]);
       if (MODE == kModeBwd && e_scale) v = ldexp(v, e_scale);
       cur[pad + l] = v;
+      if (MODE == kModeFwd) snap[l] = v;
     }
     __syncthreads();
+    stamp(3);
     if (MODE == kModeBwd && done >= total) break;
   }
+  stamp_flush();
 
   if (MODE == kModeBwd) {
     // last of the 2*S sweeps, per action: za = exp(r) * (P_a zs); pi = za / sum_a za
@@ -270,8 +350,8 @@ __global__ void __launch_bounds__(kCT) cluster_kernel(ClusterArgs a) {
         acc = fma(rv[(size_t)2 * S], q[W - 1], acc);
         acc = fma(rv[(size_t)3 * S], q[2 * W], acc);
         acc = fma(rv[(size_t)4 * S], q[0], acc);
-        za[act] = __dmul_rn(er, acc);  // rounded product, then the sum: no contraction into an fma
-        zsum = __dadd_rn(zsum, za[act]);
+        za[act] = er * acc;
+        zsum += za[act];
       }
       for (int act = 0; act < A; ++act) a.out[(iS + s) * A + act] = za[act] / zsum;
     }
@@ -317,7 +397,8 @@ static int device_cus() {
 }
 
 static size_t cluster_lds(int emax, int W) {
-  return 2 * (size_t)(emax + 2 * (W + 1)) * sizeof(double) + 2 * kTMax * sizeof(unsigned long long) + 16;
+  // two padded ping-pong buffers + the forward's block-start snapshot + summary words
+  return 2 * (size_t)(emax + 2 * (W + 1)) * sizeof(double) + (size_t)emax * sizeof(double) + 64;
 }
 
 // Tile plan for a width x height stencil grid and B instances: the fewest
@@ -394,6 +475,14 @@ int cluster_run(int mode, const ClusterPlan& p, ClusterArgs a, int B, hipStream_
     return IRLMX_EINVAL;
   }
   a.R = p.R; a.G = p.G; a.C = p.C; a.T = p.T; a.emax = p.emax; a.btot = B;
+  unsigned long long* stamps = nullptr;
+  const int nwg = p.C * std::min(p.per_launch, B);
+  if (env_int("IRLMX_STAMPS", 0)) {  // diagnostics only: phase cycle counters per workgroup
+    e = hipMallocAsync((void**)&stamps, sizeof(unsigned long long) * 8 * nwg, st);
+    if (e != hipSuccess) return hip_fail(e, "stamps alloc");
+    hipMemsetAsync(stamps, 0, sizeof(unsigned long long) * 8 * nwg, st);
+  }
+  a.stamps = stamps;
   for (int b0 = 0; b0 < B; b0 += p.per_launch) {
     const int nb = std::min(p.per_launch, B - b0);
     a.b0 = b0;
@@ -405,6 +494,18 @@ int cluster_run(int mode, const ClusterPlan& p, ClusterArgs a, int B, hipStream_
   e = hipMemcpyAsync(&err, a.err, sizeof(int), hipMemcpyDeviceToHost, st);
   if (e == hipSuccess) e = hipStreamSynchronize(st);
   if (e != hipSuccess) return hip_fail(e, "cluster sync");
+  if (stamps) {
+    unsigned long long* h = (unsigned long long*)malloc(sizeof(unsigned long long) * 8 * nwg);
+    hipMemcpy(h, stamps, sizeof(unsigned long long) * 8 * nwg, hipMemcpyDeviceToHost);
+    double acc[5] = {0, 0, 0, 0, 0};
+    for (int g = 0; g < nwg; ++g)
+      for (int k = 0; k < 5; ++k) acc[k] += (double)h[(size_t)g * 8 + k] / nwg;
+    fprintf(stderr, "[irlmx stamps] mode=%d R=%d G=%d C=%d spt=%d blocks=%.0f  cycles/block: sweeps %.0f  publish %.0f  "
+                    "barrier %.0f  refresh %.0f\n", mode, p.R, p.G, p.C, p.spt, acc[4], acc[0] / acc[4], acc[1] / acc[4],
+            acc[2] / acc[4], acc[3] / acc[4]);
+    free(h);
+    hipFree(stamps);
+  }
   if (err) { set_error("cluster: instance barrier timed out (workgroups not co-resident?)"); return IRLMX_EHIP; }
   return 0;
 }
