@@ -51,56 +51,6 @@ namespace irlmx {
 void set_error(const char* fmt, ...);
 int hip_fail(hipError_t e, const char* what);
 
-__device__ inline unsigned int ld_sc1(unsigned int* p) {
-  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-__device__ inline void st_sc1(double* p, double v) {  // write-through (sc1) 8-byte store
-  __hip_atomic_store((unsigned long long*)p, (unsigned long long)__double_as_longlong(v), __ATOMIC_RELAXED,
-                     __HIP_MEMORY_SCOPE_AGENT);
-}
-__device__ inline double ld_sc1(const double* p) {  // L1-bypassing (sc1) 8-byte load
-  return __longlong_as_double((long long)__hip_atomic_load((unsigned long long*)p, __ATOMIC_RELAXED,
-                                                           __HIP_MEMORY_SCOPE_AGENT));
-}
-
-// Arrival barrier of the C tiles of one instance, in the fence-free form of
-// MI355X_MICROARCH.md "Valid forms" (row 1): every payload byte is stored
-// write-through (sc1) and loaded with sc1 loads, every storing wave drains
-// (s_waitcnt vmcnt(0)) before the workgroup barrier, then ONE lane adds to the
-// instance's arrival counter (agent scope) and polls it with sc1 loads; the
-// other waves load after the workgroup barrier that lane joins.  Bounded by a
-// 20 s wall-clock timeout; returns false on timeout (error word set).
-__device__ inline bool instance_barrier(unsigned int* counter, unsigned int target, int* err, int* lds_flag) {
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    int abort = 0;
-    __hip_atomic_fetch_add(counter, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();  // 100 MHz
-    while (ld_sc1(counter) < target) {
-      __builtin_amdgcn_s_sleep(1);
-      if (__builtin_amdgcn_s_memrealtime() - t0 > 2000000000ull) {
-        abort = 1;
-        atomicOr(err, 1);
-        break;
-      }
-    }
-    *lds_flag = abort;
-  }
-  __syncthreads();
-  return *lds_flag == 0;
-}
-
-__device__ inline unsigned long long stamp_now() { return __builtin_amdgcn_s_memtime(); }
-
-// OR of a 32-bit value over the wave (one ballot per bit that may be set).
-__device__ inline unsigned wave_or_bits(unsigned v, int nbits) {
-  unsigned out = 0;
-  for (int b = 0; b < nbits; ++b)
-    if (__ballot((v >> b) & 1u)) out |= 1u << b;
-  return out;
-}
-
 // LDS buffer layout: [W + 1 zeros][E states][W + 1 zeros].  With the pads, the
 // five stencil reads of state l are q[0], q[W-1], q[W], q[W+1], q[2W] for
 // q = buf + l + 1: one address register per state and constant offsets (the
@@ -428,9 +378,40 @@ bool cluster_plan(int W, int H, int B, ClusterPlan* out) {
       if (cost < best - 1e-9) {
         best = cost;
         ok = true;
-        *out = ClusterPlan{R, G, C, G, std::min(per, B), spt, spt * kCT, cluster_lds(spt * kCT, W)};
+        *out = ClusterPlan{R, G, C, G, std::min(per, B), spt, spt * kCT, cluster_lds(spt * kCT, W), 0, 0, 0};
       }
     }
+  }
+  // register-resident strip kernel (IRLMX_STRIP=1): widths 64 / 128 / 256, 512 threads, 8 bands
+  if (ok && env_int("IRLMX_STRIP", 0) && (W == 64 || W == 128 || W == 256)) {
+    const int cpl = W / 64;
+    const int nb = kStripThreads / kWave;
+    static const int rpts[] = {16, 12, 8, 6, 4, 3, 2, 1};
+    double sbest = 1e300;
+    ClusterPlan sp{};
+    bool sok = false;
+    for (int rpt : rpts) {
+      if (!strip_fn<kModeFwd>(cpl, rpt)) continue;
+      const int rows = nb * rpt;
+      for (int G = kTMax; G >= 1; --G) {
+        if (fG && G != fG) continue;
+        for (int R = std::min(H, rows - 2 * G); R >= 1; --R) {
+          if (fR && R != fR) continue;
+          const int C = (H + R - 1) / R;
+          const int per = cus / C;
+          if (per < 1) continue;
+          const int nl = (B + per - 1) / per;
+          const double cost = nl * (double)(rpt * cpl) * (G + 8.0) / G;
+          if (cost < sbest - 1e-9) {
+            sbest = cost;
+            sok = true;
+            sp = ClusterPlan{R, G, C, G, std::min(per, B), rpt * cpl, rows * W, strip_lds(W, rows * W, kStripThreads),
+                             1, cpl, rpt};
+          }
+        }
+      }
+    }
+    if (sok) *out = sp;
   }
   return ok;
 }
@@ -462,12 +443,15 @@ static void* cluster_fn(int spt, int W) {
 // Launch the cluster kernel over all instances, `per_launch` at a time, then
 // check the barrier-timeout word (synchronises the stream).
 int cluster_run(int mode, const ClusterPlan& p, ClusterArgs a, int B, hipStream_t st) {
-  void* fn = mode == kModeFwd ? cluster_fn<kModeFwd>(p.spt, a.W) : cluster_fn<kModeBwd>(p.spt, a.W);
+  void* fn;
+  if (p.strip) fn = mode == kModeFwd ? strip_fn<kModeFwd>(p.cpl, p.rpt) : strip_fn<kModeBwd>(p.cpl, p.rpt);
+  else fn = mode == kModeFwd ? cluster_fn<kModeFwd>(p.spt, a.W) : cluster_fn<kModeBwd>(p.spt, a.W);
+  const int nt = p.strip ? kStripThreads : kCT;
   if (!fn) { set_error("cluster: no kernel for spt=%d", p.spt); return IRLMX_EINVAL; }
   hipError_t e = hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)p.lds);
   if (e != hipSuccess) return hip_fail(e, "cluster hipFuncSetAttribute");
   int per_cu = 0;
-  e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, (const void*)fn, kCT, p.lds);
+  e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, (const void*)fn, nt, p.lds);
   if (e != hipSuccess) return hip_fail(e, "cluster occupancy");
   const int resident = per_cu * device_cus();
   if (p.C * p.per_launch > resident) {
@@ -487,7 +471,7 @@ int cluster_run(int mode, const ClusterPlan& p, ClusterArgs a, int B, hipStream_
     const int nb = std::min(p.per_launch, B - b0);
     a.b0 = b0;
     void* args[] = {&a};
-    e = hipLaunchKernel(fn, dim3(nb * p.C), dim3(kCT), args, p.lds, st);
+    e = hipLaunchKernel(fn, dim3(nb * p.C), dim3(nt), args, p.lds, st);
     if (e != hipSuccess) return hip_fail(e, "cluster launch");
   }
   int err = 0;
@@ -500,8 +484,8 @@ int cluster_run(int mode, const ClusterPlan& p, ClusterArgs a, int B, hipStream_
     double acc[5] = {0, 0, 0, 0, 0};
     for (int g = 0; g < nwg; ++g)
       for (int k = 0; k < 5; ++k) acc[k] += (double)h[(size_t)g * 8 + k] / nwg;
-    fprintf(stderr, "[irlmx stamps] mode=%d R=%d G=%d C=%d spt=%d blocks=%.0f  cycles/block: sweeps %.0f  publish %.0f  "
-                    "barrier %.0f  refresh %.0f\n", mode, p.R, p.G, p.C, p.spt, acc[4], acc[0] / acc[4], acc[1] / acc[4],
+    fprintf(stderr, "[irlmx stamps] %s mode=%d R=%d G=%d C=%d spt=%d blocks=%.0f  cycles/block: sweeps %.0f  publish %.0f  "
+                    "barrier %.0f  refresh %.0f\n", p.strip ? "strip" : "lds", mode, p.R, p.G, p.C, p.spt, acc[4], acc[0] / acc[4], acc[1] / acc[4],
             acc[2] / acc[4], acc[3] / acc[4]);
     free(h);
     hipFree(stamps);

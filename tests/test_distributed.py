@@ -1,0 +1,110 @@
+"""Multi-process paths of the instance sharding (gloo, world size 2).
+
+CPU: shard ranges cover every instance exactly once; the timing max-reduction
+and the result gather work over gloo.  GPU: two ranks share cuda:0 and each
+runs its block of instances; the gathered result equals one process running
+the whole batch bit for bit (instances are independent; no data-path
+collective).
+"""
+
+import os
+import socket
+import subprocess
+import sys
+import textwrap
+
+import numpy as np
+import pytest
+
+from conftest import PKG_DIR, ROOT
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def test_shard_ranges_cover_all():
+    from irlmx.shard import shard_range
+    for n in (1, 7, 64, 256):
+        for world in (1, 2, 3, 8):
+            got = []
+            for r in range(world):
+                lo, hi = shard_range(n, world, r)
+                got.extend(range(lo, hi))
+            assert got == list(range(n))
+
+
+WORKER = textwrap.dedent("""
+    import os, sys, json
+    sys.path.insert(0, {pkg!r})
+    import numpy as np, torch, torch.distributed as dist
+    dist.init_process_group("gloo", init_method="tcp://127.0.0.1:{port}", rank={rank}, world_size=2)
+    from irlmx.shard import shard_range, max_over_ranks, gather_to_rank0
+    rank = dist.get_rank()
+    lo, hi = shard_range(9, 2, rank)
+    t = max_over_ranks(1.0 + rank)
+    mode = {mode!r}
+    if mode == "cpu":
+        local = torch.arange(lo, hi, dtype=torch.float64)[:, None] * torch.ones(1, 3, dtype=torch.float64)
+    else:
+        from irlmx import DeviceMDP, ops
+        from irlmx.shard import instance_slips
+        dev = torch.device("cuda", 0)
+        size = 6; n = size * size
+        mdp = DeviceMDP.icy_gridworld(size, instance_slips(np.arange(lo, hi), 9), device=dev)
+        rew = np.random.default_rng(5).uniform(0, 1, (9, n))[lo:hi]
+        tm = ops.terminal_mask([n - 1], n, batch=hi - lo, device=dev)
+        pi = ops.backward_maxent(mdp, rew, tm)
+        p0 = np.zeros((hi - lo, n)); p0[:, 0] = 1.0
+        svf, k, _ = ops.forward_svf(mdp, p0, tm, pi)
+        local = svf
+    out = gather_to_rank0(local, 9)
+    if rank == 0:
+        np.save({out!r}, out.numpy())
+        json.dump({{"tmax": t}}, open({out!r} + ".json", "w"))
+    dist.destroy_process_group()
+""")
+
+
+def _run_pair(tmp_path, mode):
+    port = _free_port()
+    out = str(tmp_path / f"gathered_{mode}.npy")
+    procs = []
+    for rank in range(2):
+        code = WORKER.format(pkg=PKG_DIR, port=port, rank=rank, mode=mode, out=out)
+        env = dict(os.environ, MASTER_ADDR="127.0.0.1")
+        procs.append(subprocess.Popen([sys.executable, "-c", code], env=env, cwd=ROOT))
+    for p in procs:
+        assert p.wait(timeout=240) == 0
+    import json
+    return np.load(out), json.load(open(out + ".json"))
+
+
+def test_gloo_gather_and_max(tmp_path):
+    got, meta = _run_pair(tmp_path, "cpu")
+    assert meta["tmax"] == 2.0
+    assert np.array_equal(got, np.arange(9.0)[:, None] * np.ones((1, 3)))
+
+
+@pytest.mark.gpu
+def test_sharded_equals_single_process(tmp_path):
+    import torch
+    import __graft_entry__ as g
+    g.build()
+    from irlmx import DeviceMDP, ops
+    from irlmx.shard import instance_slips
+    got, _ = _run_pair(tmp_path, "gpu")
+    dev = torch.device("cuda", 0)
+    size, n = 6, 36
+    mdp = DeviceMDP.icy_gridworld(size, instance_slips(np.arange(9), 9), device=dev)
+    rew = np.random.default_rng(5).uniform(0, 1, (9, n))
+    tm = ops.terminal_mask([n - 1], n, batch=9, device=dev)
+    pi = ops.backward_maxent(mdp, rew, tm)
+    p0 = np.zeros((9, n))
+    p0[:, 0] = 1.0
+    svf, _, _ = ops.forward_svf(mdp, p0, tm, pi)
+    assert np.array_equal(got, svf.cpu().numpy())
