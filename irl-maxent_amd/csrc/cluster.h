@@ -9,6 +9,8 @@
 namespace irlmx {
 
 constexpr int kCT = 1024;    // threads per cluster workgroup
+constexpr int kPairThreads = 512;  // threads per workgroup of the pair layout
+constexpr int kSptMaxPair = 12;    // states per thread of the pair layout
 constexpr int kTMax = 16;    // max sweeps per block (= max ghost rows)
 constexpr int kSptMax = 6;   // states per thread -> extended tile <= 6144 states (no VGPR spills)
 constexpr int kStripThreads = 512;  // strip kernel workgroup (2 waves per SIMD, 256 VGPRs)
@@ -46,6 +48,7 @@ struct ClusterPlan {
   int R, G, C, T, per_launch, spt, emax;
   size_t lds;
   int strip, cpl, rpt;  // strip kernel (strip.hip) shape; strip == 0: LDS kernel
+  bool pair;            // LDS kernel with the pair layout (widths 64 / 128)
 };
 
 size_t strip_lds(int W, int emax, int nt);

@@ -63,8 +63,26 @@ int hip_fail(hipError_t e, const char* what);
 // |delta| is NaN" (bit 16 + i).  Threads collect them in a register, and the
 // tile ORs them once per block (ballots, one LDS atomic per wave, one global
 // atomic per tile) -- no per-sweep reduction.
-template <int MODE, int SPT, int WT>
-__global__ void __launch_bounds__(kCT) cluster_kernel(ClusterArgs a) {
+//
+// PAIR (widths 64 and 128): thread slot jp holds the horizontally adjacent
+// states 2p, 2p + 1 (p = tid + jp * NT) and keeps their values in registers
+// between sweeps.  A wave then spans 64 consecutive pairs, so the horizontal
+// neighbours of a pair are the neighbouring lanes' registers (DPP wave shifts;
+// at a row edge the neighbour lane belongs to another row or is zero-filled,
+// and the stencil weight there is 0), and each sweep reads only the pairs
+// above and below (two ds_read_b128) and writes its own (one ds_write_b128):
+// a third of the LDS traffic of the per-state form.
+template <int CTRL>
+__device__ inline double dpp_shift_f64(double x) {
+  const long long b = __double_as_longlong(x);
+  const int lo = __builtin_amdgcn_update_dpp(0, (int)(b & 0xffffffffLL), CTRL, 0xF, 0xF, true);
+  const int hi = __builtin_amdgcn_update_dpp(0, (int)(b >> 32), CTRL, 0xF, 0xF, true);
+  return __longlong_as_double(((long long)hi << 32) | (long long)(unsigned)lo);
+}
+
+template <int MODE, int SPT, int WT, bool PAIR, int NT>
+__global__ void __launch_bounds__(NT) cluster_kernel(ClusterArgs a) {
+  static_assert(!PAIR || (SPT % 2 == 0 && (WT == 64 || WT == 128)), "pair layout: even SPT, width 64/128");
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   const int W = WT ? WT : a.W;
   const int H = a.H, S = a.S;
@@ -78,8 +96,10 @@ __global__ void __launch_bounds__(kCT) cluster_kernel(ClusterArgs a) {
   // owned rows other tiles read as ghosts: within G rows of either tile edge
   const int pubA1 = min(own1, own0 + a.G * W), pubB0 = max(pubA1, own1 - a.G * W);
   const int base = e0 * W;
-  const int pad = W + 1;
+  const int pad = PAIR ? W : W + 1;  // pair layout keeps every pair 16-byte aligned
   const int blen = a.emax + 2 * pad;
+  // state index of register slot j
+  auto slot_state = [&](int j) { return PAIR ? 2 * (tid + (j >> 1) * NT) + (j & 1) : tid + j * NT; };
   double* bufA = (double*)smem;
   double* bufB = bufA + blen;
   double* snap = bufB + blen;                                            // forward: block-start state
@@ -89,7 +109,7 @@ __global__ void __launch_bounds__(kCT) cluster_kernel(ClusterArgs a) {
   const size_t iS = (size_t)inst * S;
   if (MODE == kModeFwd && a.bad[inst]) {
     // non-finite policy: the reference's dense product is NaN after one sweep
-    for (int l = own0 + tid; l < own1; l += kCT) a.out[iS + base + l] = __longlong_as_double(0x7ff8000000000000LL);
+    for (int l = own0 + tid; l < own1; l += NT) a.out[iS + base + l] = __longlong_as_double(0x7ff8000000000000LL);
     if (tile == 0 && tid == 0) { a.iters[inst] = 1; a.status[inst] = IRLMX_NONFINITE; }
     return;
   }
@@ -100,7 +120,7 @@ __global__ void __launch_bounds__(kCT) cluster_kernel(ClusterArgs a) {
   const size_t wbase = (MODE == kModeBwd && a.tab_shared) ? 0 : iS * kStencilK;
 #pragma unroll
   for (int j = 0; j < SPT; ++j) {
-    const int l = tid + j * kCT;
+    const int l = slot_state(j);
     c0[j] = 0.0;
 #pragma unroll
     for (int k = 0; k < kStencilK; ++k) w[j][k] = 0.0;
@@ -116,9 +136,9 @@ __global__ void __launch_bounds__(kCT) cluster_kernel(ClusterArgs a) {
     for (int k = 0; k < kStencilK; ++k) asm volatile("" : "+v"(w[j][k]));
     asm volatile("" : "+v"(c0[j]));
   }
-  for (int i = tid; i < 2 * blen; i += kCT) bufA[i] = 0.0;
+  for (int i = tid; i < 2 * blen; i += NT) bufA[i] = 0.0;
   __syncthreads();
-  for (int l = tid; l < E; l += kCT) {
+  for (int l = tid; l < E; l += NT) {
     double v0 = 0.0;
     if (MODE == kModeBwd) v0 = a.term[iS + base + l] ? 1.0 : 0.0;
     bufA[pad + l] = v0;
@@ -127,6 +147,19 @@ __global__ void __launch_bounds__(kCT) cluster_kernel(ClusterArgs a) {
   }
   if (tid < 2) red[tid] = 0ull;
   if (tid == 0) lflag[0] = 0;
+  double cv[PAIR ? SPT : 1];  // pair layout: this thread's states, kept across sweeps
+#pragma unroll
+  for (int j = 0; j < (PAIR ? SPT : 1); ++j) {
+    const int l = slot_state(j);
+    cv[j] = (PAIR && MODE == kModeBwd && l < E) ? (a.term[iS + base + l] ? 1.0 : 0.0) : 0.0;
+  }
+  // reload the register copy from an LDS buffer (after a ghost refresh or a rollback)
+  auto reload = [&](const double* buf) {
+    if (PAIR) {
+#pragma unroll
+      for (int j = 0; j < (PAIR ? SPT : 1); ++j) cv[j] = buf[pad + slot_state(j)];
+    }
+  };
 
   int T = a.T;
   if (MODE == kModeBwd) {
@@ -143,25 +176,14 @@ __global__ void __launch_bounds__(kCT) cluster_kernel(ClusterArgs a) {
   // One Jacobi sweep over the extended tile.  Forward: sets bit i / 16 + i of
   // `flags` for an owned |delta| > eps / NaN.  Backward: when `want_max`,
   // returns this thread's max over owned states (for the block-end rescale).
-  // Every slot l < SPT * kCT is swept, also l >= E: those have zero weights and
+  // Every slot l < SPT * NT is swept, also l >= E: those have zero weights and
   // zero c0, read only zeros (buffers are zero-filled and hold emax + 2 pads),
   // and stay 0 -- which is what state E - 1's down-neighbour must read.  No
   // per-state branch, so all LDS reads of a sweep can be in flight together.
   auto sweep = [&](const double* __restrict__ din, double* __restrict__ dout, int i, unsigned& flags,
                    bool want_max) {
     unsigned long long mx = 0ull;
-#pragma unroll
-    for (int j = 0; j < SPT; ++j) {
-      const int l = tid + j * kCT;
-      const double* q = din + l + 1;
-      const double self = q[W];
-      double acc = fma(w[j][0], self, 0.0);
-      acc = fma(w[j][1], q[W + 1], acc);
-      acc = fma(w[j][2], q[W - 1], acc);
-      acc = fma(w[j][3], q[2 * W], acc);
-      acc = fma(w[j][4], q[0], acc);
-      const double nv = MODE == kModeFwd ? c0[j] + acc : c0[j] * acc;
-      dout[pad + l] = nv;
+    auto account = [&](int l, double nv, double self) {
       if (l >= own0 && l < own1) {
         if (MODE == kModeFwd) {
           const double d = fabs(nv - self);
@@ -171,6 +193,51 @@ __global__ void __launch_bounds__(kCT) cluster_kernel(ClusterArgs a) {
           const unsigned long long d = abs_bits(nv);
           mx = d > mx ? d : mx;
         }
+      }
+    };
+    if (PAIR) {
+#pragma unroll
+      for (int jp = 0; jp < SPT / 2; ++jp) {
+        const int l = 2 * (tid + jp * NT);
+        const double2 up = *reinterpret_cast<const double2*>(din + l);           // row above (pad = W)
+        const double2 dn = *reinterpret_cast<const double2*>(din + 2 * W + l);   // row below
+        const double va = cv[2 * jp], vb = cv[2 * jp + 1];
+        const double lft = dpp_shift_f64<0x138>(vb);  // wave_shr1: left neighbour of state a
+        const double rgt = dpp_shift_f64<0x130>(va);  // wave_shl1: right neighbour of state b
+        const double* wa = w[2 * jp];
+        const double* wb = w[2 * jp + 1];
+        double acc = fma(wa[0], va, 0.0);
+        acc = fma(wa[1], vb, acc);
+        acc = fma(wa[2], lft, acc);
+        acc = fma(wa[3], dn.x, acc);
+        acc = fma(wa[4], up.x, acc);
+        const double na = MODE == kModeFwd ? c0[2 * jp] + acc : c0[2 * jp] * acc;
+        acc = fma(wb[0], vb, 0.0);
+        acc = fma(wb[1], rgt, acc);
+        acc = fma(wb[2], va, acc);
+        acc = fma(wb[3], dn.y, acc);
+        acc = fma(wb[4], up.y, acc);
+        const double nb = MODE == kModeFwd ? c0[2 * jp + 1] + acc : c0[2 * jp + 1] * acc;
+        *reinterpret_cast<double2*>(dout + W + l) = make_double2(na, nb);
+        account(l, na, va);
+        account(l + 1, nb, vb);
+        cv[2 * jp] = na;
+        cv[2 * jp + 1] = nb;
+      }
+    } else {
+#pragma unroll
+      for (int j = 0; j < SPT; ++j) {
+        const int l = tid + j * NT;
+        const double* q = din + l + 1;
+        const double self = q[W];
+        double acc = fma(w[j][0], self, 0.0);
+        acc = fma(w[j][1], q[W + 1], acc);
+        acc = fma(w[j][2], q[W - 1], acc);
+        acc = fma(w[j][3], q[2 * W], acc);
+        acc = fma(w[j][4], q[0], acc);
+        const double nv = MODE == kModeFwd ? c0[j] + acc : c0[j] * acc;
+        dout[pad + l] = nv;
+        account(l, nv, self);
       }
     }
     __syncthreads();
@@ -217,8 +284,8 @@ __global__ void __launch_bounds__(kCT) cluster_kernel(ClusterArgs a) {
     }
     // ---- publish halo rows (write-through), combine the summaries, arrive ----
     double* pubm = a.pub + (size_t)(m & 1) * pubStride + iS;
-    for (int l = own0 + tid; l < pubA1; l += kCT) st_sc1(&pubm[base + l], cur[pad + l]);
-    for (int l = pubB0 + tid; l < own1; l += kCT) st_sc1(&pubm[base + l], cur[pad + l]);
+    for (int l = own0 + tid; l < pubA1; l += NT) st_sc1(&pubm[base + l], cur[pad + l]);
+    for (int l = pubB0 + tid; l < own1; l += NT) st_sc1(&pubm[base + l], cur[pad + l]);
     __syncthreads();  // the tile summary in red[m & 1] is complete
     if (tid == 0) {
       const unsigned long long v = red[m & 1];
@@ -247,14 +314,15 @@ __global__ void __launch_bounds__(kCT) cluster_kernel(ClusterArgs a) {
       }
       if (conv) {
         // exact stop inside the block: replay `conv` sweeps from the block-start state
-        for (int l = tid; l < E; l += kCT) cur[pad + l] = snap[l];
+        for (int l = tid; l < E; l += NT) cur[pad + l] = snap[l];
         __syncthreads();
+        reload(cur);
         unsigned scratch = 0;
         for (int i = 0; i < conv; ++i) {
           sweep(cur, oth, i, scratch, false);
           double* t = cur; cur = oth; oth = t;
         }
-        for (int l = own0 + tid; l < own1; l += kCT) a.out[iS + base + l] = cur[pad + l];
+        for (int l = own0 + tid; l < own1; l += NT) a.out[iS + base + l] = cur[pad + l];
         stamp(3);
         stamp_flush();
         if (tile == 0 && tid == 0) {
@@ -271,13 +339,14 @@ __global__ void __launch_bounds__(kCT) cluster_kernel(ClusterArgs a) {
     if (MODE == kModeBwd && a.rescale)
       e_scale = rescale_exponent(bits_double(
           __hip_atomic_load(&slots64[(m % 3) + 3], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)));
-    for (int l = tid; l < E; l += kCT) {
+    for (int l = tid; l < E; l += NT) {
       double v = (l >= own0 && l < own1) ? cur[pad + l] : ld_sc1(&pubm[base + l]);
       if (MODE == kModeBwd && e_scale) v = ldexp(v, e_scale);
       cur[pad + l] = v;
       if (MODE == kModeFwd) snap[l] = v;
     }
     __syncthreads();
+    reload(cur);
     stamp(3);
     if (MODE == kModeBwd && done >= total) break;
   }
@@ -287,9 +356,9 @@ __global__ void __launch_bounds__(kCT) cluster_kernel(ClusterArgs a) {
     // last of the 2*S sweeps, per action: za = exp(r) * (P_a zs); pi = za / sum_a za
     const int A = a.A;
     const size_t tb = a.tab_shared ? 0 : (size_t)inst;
-    for (int l = own0 + tid; l < own1; l += kCT) {
+    for (int l = own0 + tid; l < own1; l += NT) {
       const int s = base + l;
-      const double* q = cur + l + 1;
+      const double* q = cur + l + (pad - W);
       const double er = exp(a.vin[iS + s]);
       double za[8];
       double zsum = 0.0;
@@ -358,8 +427,12 @@ bool cluster_plan(int W, int H, int B, ClusterPlan* out) {
   if (env_int("IRLMX_CLUSTER", 1) == 0) return false;
   const int cus = device_cus();
   if (cus <= 0) return false;
-  const int rows_cap = kCT * kSptMax / W;
   const int fR = env_int("IRLMX_CLUSTER_R", 0), fG = env_int("IRLMX_CLUSTER_G", 0);
+  // pair layout (cluster_kernel PAIR) for widths 64 / 128 unless IRLMX_PAIR=0
+  const bool pair = (W == 64 || W == 128) && env_int("IRLMX_PAIR", 1) != 0;
+  const int nt = pair ? kPairThreads : kCT;
+  const int spt_max = pair ? kSptMaxPair : kSptMax;
+  const int rows_cap = nt * spt_max / W;
   double best = 1e300;
   bool ok = false;
   for (int G = kTMax; G >= 1; --G) {
@@ -369,8 +442,9 @@ bool cluster_plan(int W, int H, int B, ClusterPlan* out) {
       const int C = (H + R - 1) / R;
       const int ext = std::min(H, R + 2 * G);
       const int E = ext * W;
-      const int spt = (E + kCT - 1) / kCT;
-      if (spt > kSptMax) continue;
+      int spt = (E + nt - 1) / nt;
+      if (pair && (spt & 1)) ++spt;
+      if (spt > spt_max) continue;
       const int per = cus / C;
       if (per < 1) continue;
       const int nl = (B + per - 1) / per;
@@ -378,7 +452,7 @@ bool cluster_plan(int W, int H, int B, ClusterPlan* out) {
       if (cost < best - 1e-9) {
         best = cost;
         ok = true;
-        *out = ClusterPlan{R, G, C, G, std::min(per, B), spt, spt * kCT, cluster_lds(spt * kCT, W), 0, 0, 0};
+        *out = ClusterPlan{R, G, C, G, std::min(per, B), spt, spt * nt, cluster_lds(spt * nt, W), 0, 0, 0, pair};
       }
     }
   }
@@ -406,7 +480,7 @@ bool cluster_plan(int W, int H, int B, ClusterPlan* out) {
             sbest = cost;
             sok = true;
             sp = ClusterPlan{R, G, C, G, std::min(per, B), rpt * cpl, rows * W, strip_lds(W, rows * W, kStripThreads),
-                             1, cpl, rpt};
+                             1, cpl, rpt, false};
           }
         }
       }
@@ -419,19 +493,38 @@ bool cluster_plan(int W, int H, int B, ClusterPlan* out) {
 template <int MODE, int WT>
 static void* cluster_fn_w(int spt) {
   switch (spt) {
-    case 1: return (void*)&cluster_kernel<MODE, 1, WT>;
-    case 2: return (void*)&cluster_kernel<MODE, 2, WT>;
-    case 3: return (void*)&cluster_kernel<MODE, 3, WT>;
-    case 4: return (void*)&cluster_kernel<MODE, 4, WT>;
-    case 5: return (void*)&cluster_kernel<MODE, 5, WT>;
-    case 6: return (void*)&cluster_kernel<MODE, 6, WT>;
+    case 1: return (void*)&cluster_kernel<MODE, 1, WT, false, kCT>;
+    case 2: return (void*)&cluster_kernel<MODE, 2, WT, false, kCT>;
+    case 3: return (void*)&cluster_kernel<MODE, 3, WT, false, kCT>;
+    case 4: return (void*)&cluster_kernel<MODE, 4, WT, false, kCT>;
+    case 5: return (void*)&cluster_kernel<MODE, 5, WT, false, kCT>;
+    case 6: return (void*)&cluster_kernel<MODE, 6, WT, false, kCT>;
   }
   return nullptr;
 }
 
-// grid widths with compile-time LDS offsets; any other width uses WT = 0
+template <int MODE, int WT>
+static void* cluster_fn_pair(int spt) {
+  switch (spt) {
+    case 2: return (void*)&cluster_kernel<MODE, 2, WT, true, kPairThreads>;
+    case 4: return (void*)&cluster_kernel<MODE, 4, WT, true, kPairThreads>;
+    case 6: return (void*)&cluster_kernel<MODE, 6, WT, true, kPairThreads>;
+    case 8: return (void*)&cluster_kernel<MODE, 8, WT, true, kPairThreads>;
+    case 10: return (void*)&cluster_kernel<MODE, 10, WT, true, kPairThreads>;
+    case 12: return (void*)&cluster_kernel<MODE, 12, WT, true, kPairThreads>;
+  }
+  return nullptr;
+}
+
+// pair layout for widths 64 / 128 (even states per thread); compile-time LDS
+// offsets for widths 64 / 128 / 256; any other width uses WT = 0
 template <int MODE>
-static void* cluster_fn(int spt, int W) {
+static void* cluster_fn(int spt, int W, bool pair) {
+  if (pair) {
+    if (W == 64) return cluster_fn_pair<MODE, 64>(spt);
+    if (W == 128) return cluster_fn_pair<MODE, 128>(spt);
+    return nullptr;
+  }
   switch (W) {
     case 64: return cluster_fn_w<MODE, 64>(spt);
     case 128: return cluster_fn_w<MODE, 128>(spt);
@@ -445,8 +538,8 @@ static void* cluster_fn(int spt, int W) {
 int cluster_run(int mode, const ClusterPlan& p, ClusterArgs a, int B, hipStream_t st) {
   void* fn;
   if (p.strip) fn = mode == kModeFwd ? strip_fn<kModeFwd>(p.cpl, p.rpt) : strip_fn<kModeBwd>(p.cpl, p.rpt);
-  else fn = mode == kModeFwd ? cluster_fn<kModeFwd>(p.spt, a.W) : cluster_fn<kModeBwd>(p.spt, a.W);
-  const int nt = p.strip ? kStripThreads : kCT;
+  else fn = mode == kModeFwd ? cluster_fn<kModeFwd>(p.spt, a.W, p.pair) : cluster_fn<kModeBwd>(p.spt, a.W, p.pair);
+  const int nt = p.strip ? kStripThreads : (p.pair ? kPairThreads : kCT);
   if (!fn) { set_error("cluster: no kernel for spt=%d", p.spt); return IRLMX_EINVAL; }
   hipError_t e = hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)p.lds);
   if (e != hipSuccess) return hip_fail(e, "cluster hipFuncSetAttribute");
@@ -484,8 +577,8 @@ int cluster_run(int mode, const ClusterPlan& p, ClusterArgs a, int B, hipStream_
     double acc[5] = {0, 0, 0, 0, 0};
     for (int g = 0; g < nwg; ++g)
       for (int k = 0; k < 5; ++k) acc[k] += (double)h[(size_t)g * 8 + k] / nwg;
-    fprintf(stderr, "[irlmx stamps] %s mode=%d R=%d G=%d C=%d spt=%d blocks=%.0f  cycles/block: sweeps %.0f  publish %.0f  "
-                    "barrier %.0f  refresh %.0f\n", p.strip ? "strip" : "lds", mode, p.R, p.G, p.C, p.spt, acc[4], acc[0] / acc[4], acc[1] / acc[4],
+    fprintf(stderr, "[irlmx stamps] %s%s mode=%d R=%d G=%d C=%d spt=%d blocks=%.0f  cycles/block: sweeps %.0f  publish %.0f  "
+                    "barrier %.0f  refresh %.0f\n", p.strip ? "strip" : "lds", p.pair ? "-pair" : "", mode, p.R, p.G, p.C, p.spt, acc[4], acc[0] / acc[4], acc[1] / acc[4],
             acc[2] / acc[4], acc[3] / acc[4]);
     free(h);
     hipFree(stamps);

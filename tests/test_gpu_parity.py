@@ -334,3 +334,41 @@ def test_shapes_bit_identical(dev, monkeypatch):
             assert torch.equal(out["fused"][0], out[name][0]), (size, name, "pi")
             assert torch.equal(out["fused"][1], out[name][1]), (size, name, "svf")
             assert out["fused"][2] == out[name][2], (size, name)
+
+
+@pytest.mark.gpu
+def test_pair_layout_bit_identical(dev, monkeypatch):
+    """The pair layout of the cluster kernel (widths 64 / 128: two states per
+    register slot, horizontal neighbours by DPP lane shifts) computes the same
+    float64 operations as the per-state LDS layout and the per-sweep shape, so
+    policies, SVFs and sweep counts agree bit for bit -- with the planner's tiles
+    and with forced small tiles (more halo exchanges, in-block rollback)."""
+    from irlmx import DeviceMDP, ops
+    keys = ("IRLMX_FUSED_MAX_STATES", "IRLMX_CLUSTER", "IRLMX_CLUSTER_R", "IRLMX_CLUSTER_G", "IRLMX_PAIR")
+    shapes = {"sweep": {"IRLMX_FUSED_MAX_STATES": "0", "IRLMX_CLUSTER": "0"},
+              "lds": {"IRLMX_FUSED_MAX_STATES": "0", "IRLMX_PAIR": "0"},
+              "pair": {"IRLMX_FUSED_MAX_STATES": "0"},
+              "pair_small": {"IRLMX_FUSED_MAX_STATES": "0", "IRLMX_CLUSTER_R": "7", "IRLMX_CLUSTER_G": "3"}}
+    rng = np.random.default_rng(5)
+    for size, theta, cap in ((64, "ones", 20000), (64, "unif", 0), (128, "unif", 3000)):
+        n = size * size
+        r = np.ones(n) if theta == "ones" else rng.uniform(0, 1.5, n)
+        p0 = np.zeros(n)
+        p0[0] = 1.0
+        mdp = DeviceMDP.icy_gridworld(size, 0.2, device=dev)
+        tm = ops.terminal_mask([n - 1], n, device=dev)
+        out = {}
+        for name, env in shapes.items():
+            for k in keys:
+                monkeypatch.delenv(k, raising=False)
+            for k, v in env.items():
+                monkeypatch.setenv(k, v)
+            pi = ops.backward_maxent(mdp, r, tm)
+            svf, k, _ = ops.forward_svf(mdp, p0, tm, pi, max_iter=cap)
+            out[name] = (pi, svf, int(k[0]))
+        for k in keys:
+            monkeypatch.delenv(k, raising=False)
+        for name in ("lds", "pair", "pair_small"):
+            assert torch.equal(out["sweep"][0], out[name][0]), (size, theta, name, "pi")
+            assert torch.equal(out["sweep"][1], out[name][1]), (size, theta, name, "svf")
+            assert out["sweep"][2] == out[name][2], (size, theta, name)
