@@ -34,7 +34,11 @@ struct ClusterArgs {
   long long max_iter;
   long long n_sweeps;      // backward: collapsed sweeps (2S - 1)
   int rescale;
-  double* pub;             // [2][B][S]
+  double* pub;             // strip kernel: [2][B][S]
+  unsigned long long* gran;   // LDS kernel: [B][2][S] x 16-byte tagged granule pairs (halo rows)
+  unsigned long long* sgran;  // LDS kernel: [B][3][H] x 16-byte tagged granule pairs (tile summaries, XCC ids)
+  int xcd_group;           // LDS kernel: number the tiles of an instance within one XCD group
+  unsigned salt;           // LDS kernel: per-launch granule tag salt
   unsigned long long* slots;  // [B][3][kTMax]
   unsigned int* counter;   // [B]
   int* err;                // [1] barrier timeout
@@ -65,6 +69,54 @@ __device__ inline void st_sc1(double* p, double v) {  // write-through (sc1) 8-b
 __device__ inline double ld_sc1(const double* p) {  // L1-bypassing (sc1) 8-byte load
   return __longlong_as_double((long long)__hip_atomic_load((unsigned long long*)p, __ATOMIC_RELAXED,
                                                            __HIP_MEMORY_SCOPE_AGENT));
+}
+
+// Tagged granules (cdna_hip_programming.md Guideline 16, form R2: the data is
+// the flag).  A 64-bit value v travels as one 16-byte sc1 store of
+// {lo32(v), tag, hi32(v), tag}; each 8-byte half is an untorn {value, tag}
+// granule, so a reader that sees tag == the block's epoch in both halves (sc1
+// loads: L1 bypassed, no acquire needed) holds the value of that block.  No
+// counter, no fence, one fabric round trip per exchange.  Epoch = block + 1;
+// the workspace is zeroed before every call, so no stale tag can match.
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+constexpr int kGatherPerThread = 4;
+
+__device__ inline __amdgpu_buffer_rsrc_t gran_rsrc(const void* base, unsigned bytes) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), 0, (int)bytes, 0x00020000);
+}
+__device__ inline unsigned long long dbits(double v) { return (unsigned long long)__double_as_longlong(v); }
+// sc1 (write-through) store, or a plain store when every reader shares this XCD's L2
+__device__ inline void gran_store(__amdgpu_buffer_rsrc_t r, unsigned off, unsigned long long v, unsigned tag,
+                                  bool plain) {
+  const u32x4 x = {(unsigned)v, tag, (unsigned)(v >> 32), tag};
+  if (plain) __builtin_amdgcn_raw_buffer_store_b128(x, r, (int)off, 0, 0);
+  else __builtin_amdgcn_raw_buffer_store_b128(x, r, (int)off, 0, 16 /* sc1 */);
+}
+// Poll the granule pairs selected by `want` (bit k: entry k; the last entry
+// through rsrc `rl`, the others through `r`) until all carry `tag`; false
+// after 20 s.  Every pending load of a pass is in flight at once.
+template <int N>
+__device__ inline bool gran_gather(__amdgpu_buffer_rsrc_t r, __amdgpu_buffer_rsrc_t rl, const unsigned (&off)[N],
+                                   unsigned want, unsigned tag, unsigned long long (&v)[N]) {
+  unsigned pending = want;
+  const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+  while (pending) {
+    u32x4 x[N];
+#pragma unroll
+    for (int k = 0; k < N; ++k)
+      if ((pending >> k) & 1u)
+        x[k] = __builtin_amdgcn_raw_buffer_load_b128(k == N - 1 ? rl : r, (int)off[k], 0, 16 /* sc1 */);
+#pragma unroll
+    for (int k = 0; k < N; ++k)
+      if (((pending >> k) & 1u) && x[k].y == tag && x[k].w == tag) {
+        v[k] = ((unsigned long long)x[k].z << 32) | x[k].x;
+        pending &= ~(1u << k);
+      }
+    if (!pending) break;
+    if (__builtin_amdgcn_s_memrealtime() - t0 > 2000000000ull) return false;
+    __builtin_amdgcn_s_sleep(1);
+  }
+  return true;
 }
 
 // Arrival barrier of the C tiles of one instance, in the fence-free form of
@@ -103,6 +155,39 @@ __device__ inline unsigned wave_or_bits(unsigned v, int nbits) {
   for (int b = 0; b < nbits; ++b)
     if (__ballot((v >> b) & 1u)) out |= 1u << b;
   return out;
+}
+
+// Backward rescale summary as a 32-bit code, monotone in |m|: 0 for m == 0,
+// kCodeNonFinite for inf / NaN, else frexp exponent + kCodeBias.  The max of
+// codes is the code of the max, and code_exponent(code(max)) ==
+// rescale_exponent(max) (common.h), so tiles can combine codes instead of
+// 64-bit maxima.
+constexpr unsigned kCodeBias = 1100u, kCodeNonFinite = 0x1FFFu;
+__device__ inline unsigned scale_code(double m) {
+  if (!isfinite(m)) return kCodeNonFinite;  // inf or NaN (checked first: NaN > 0 is false)
+  if (!(m > 0.0)) return 0u;
+  int e;
+  frexp(m, &e);
+  return (unsigned)(e + (int)kCodeBias);
+}
+__device__ inline int code_exponent(unsigned c) {
+  return (c == 0u || c == kCodeNonFinite) ? 0 : -((int)c - (int)kCodeBias);
+}
+// max over the wave of a 13-bit code: bitwise search with ballots (no LDS)
+__device__ inline unsigned wave_max_code(unsigned c) {
+  unsigned r = 0;
+#pragma unroll
+  for (int b = 12; b >= 0; --b) {
+    const unsigned t = r | (1u << b);
+    if (__ballot(c >= t)) r = t;
+  }
+  return r;
+}
+
+__device__ inline unsigned long long wave_or_u64(unsigned long long v) {
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) v |= __shfl_xor(v, off, kWave);
+  return v;
 }
 
 bool cluster_plan(int W, int H, int B, ClusterPlan* out);

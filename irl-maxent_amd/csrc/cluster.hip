@@ -39,6 +39,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <atomic>
 #include <cmath>
 #include <cstdio>
 #include <cstdlib>
@@ -86,8 +87,14 @@ __global__ void __launch_bounds__(NT) cluster_kernel(ClusterArgs a) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   const int W = WT ? WT : a.W;
   const int H = a.H, S = a.S;
-  const int tile = blockIdx.x % a.C;
-  const int inst = a.b0 + blockIdx.x / a.C;
+  // XCD-grouped numbering (a.xcd_group): workgroups are dealt round-robin over
+  // the 8 XCDs, so blockIdx % 8 names an XCD group; the C tiles of an instance
+  // are taken from one group, which lets their halo hand-offs stay inside one
+  // L2 when the dealing is as observed (verified at run time below; speed only)
+  int lin = blockIdx.x;
+  if (a.xcd_group) lin = (blockIdx.x % 8) * (gridDim.x / 8) + blockIdx.x / 8;
+  const int tile = lin % a.C;
+  const int inst = a.b0 + lin / a.C;
   const int tid = threadIdx.x;
   const int r0 = tile * a.R, r1 = min(H, r0 + a.R);
   const int e0 = max(0, r0 - a.G), e1 = min(H, r1 + a.G);
@@ -103,8 +110,8 @@ __global__ void __launch_bounds__(NT) cluster_kernel(ClusterArgs a) {
   double* bufA = (double*)smem;
   double* bufB = bufA + blen;
   double* snap = bufB + blen;                                            // forward: block-start state
-  unsigned long long* red = (unsigned long long*)(snap + (MODE == kModeFwd ? a.emax : 0));  // [2]
-  int* lflag = (int*)(red + 2);                                          // [4]
+  unsigned long long* red = (unsigned long long*)(snap + (MODE == kModeFwd ? a.emax : 0));  // [3]
+  int* lflag = (int*)(red + 3);                                          // [4]
 
   const size_t iS = (size_t)inst * S;
   if (MODE == kModeFwd && a.bad[inst]) {
@@ -145,7 +152,7 @@ __global__ void __launch_bounds__(NT) cluster_kernel(ClusterArgs a) {
     bufB[pad + l] = v0;
     if (MODE == kModeFwd) snap[l] = v0;
   }
-  if (tid < 2) red[tid] = 0ull;
+  if (tid < 3) red[tid] = 0ull;
   if (tid == 0) lflag[0] = 0;
   double cv[PAIR ? SPT : 1];  // pair layout: this thread's states, kept across sweeps
 #pragma unroll
@@ -160,6 +167,17 @@ __global__ void __launch_bounds__(NT) cluster_kernel(ClusterArgs a) {
       for (int j = 0; j < (PAIR ? SPT : 1); ++j) cv[j] = buf[pad + slot_state(j)];
     }
   };
+
+  // per-slot predicates as bit masks (bit j: register slot j)
+  unsigned own_bits = 0, pub_bits = 0, ext_bits = 0;
+#pragma unroll
+  for (int j = 0; j < SPT; ++j) {
+    const int l = slot_state(j);
+    const bool own = l >= own0 && l < own1;
+    own_bits |= (own ? 1u : 0u) << j;
+    ext_bits |= (l < E ? 1u : 0u) << j;
+    pub_bits |= (((l >= own0 && l < pubA1) || (l >= pubB0 && l < own1)) ? 1u : 0u) << j;
+  }
 
   int T = a.T;
   if (MODE == kModeBwd) {
@@ -183,8 +201,10 @@ __global__ void __launch_bounds__(NT) cluster_kernel(ClusterArgs a) {
   auto sweep = [&](const double* __restrict__ din, double* __restrict__ dout, int i, unsigned& flags,
                    bool want_max) {
     unsigned long long mx = 0ull;
-    auto account = [&](int l, double nv, double self) {
-      if (l >= own0 && l < own1) {
+    unsigned ob = own_bits;
+    asm volatile("" : "+v"(ob));  // opaque: the per-slot predicates stay a VGPR, not hoisted SGPR masks
+    auto account = [&](int j, double nv, double self) {
+      if ((ob >> j) & 1u) {
         if (MODE == kModeFwd) {
           const double d = fabs(nv - self);
           flags |= ((d > eps) ? 1u : 0u) << i;
@@ -219,8 +239,8 @@ __global__ void __launch_bounds__(NT) cluster_kernel(ClusterArgs a) {
         acc = fma(wb[4], up.y, acc);
         const double nb = MODE == kModeFwd ? c0[2 * jp + 1] + acc : c0[2 * jp + 1] * acc;
         *reinterpret_cast<double2*>(dout + W + l) = make_double2(na, nb);
-        account(l, na, va);
-        account(l + 1, nb, vb);
+        account(2 * jp, na, va);
+        account(2 * jp + 1, nb, vb);
         cv[2 * jp] = na;
         cv[2 * jp + 1] = nb;
       }
@@ -237,21 +257,51 @@ __global__ void __launch_bounds__(NT) cluster_kernel(ClusterArgs a) {
         acc = fma(w[j][4], q[0], acc);
         const double nv = MODE == kModeFwd ? c0[j] + acc : c0[j] * acc;
         dout[pad + l] = nv;
-        account(l, nv, self);
+        account(j, nv, self);
       }
     }
     __syncthreads();
     return mx;
   };
 
-  unsigned int* slots = (unsigned int*)(a.slots + (size_t)inst * 3 * kTMax);  // [3] words (fwd masks / bwd max)
-  unsigned long long* slots64 = a.slots + (size_t)inst * 3 * kTMax;
-  const size_t pubStride = (size_t)a.btot * S;  // pub[parity] stride
+  // Halo exchange in tagged granules (cluster.h): this instance's region of
+  // a.gran is [2 parities][S states] x 16 B, of a.sgran [2][H tiles] x 16 B.
+  const __amdgpu_buffer_rsrc_t rg = gran_rsrc(a.gran + (size_t)inst * 4 * S, 32u * (unsigned)S);
+  const __amdgpu_buffer_rsrc_t rs = gran_rsrc(a.sgran + (size_t)inst * 6 * a.H, 48u * (unsigned)a.H);
+  const int ng0 = own0, ng = own0 + (E - own1);  // ghost states: [0, own0) and [own1, E)
+  const unsigned salt = (a.salt & 0xFFFu) << 20;  // per call: a stale granule of an earlier call never matches
+  // Hand-off store form: write-through (sc1) in general; plain stores (kept in
+  // the XCD's L2, where the readers' sc1 loads are served) when every tile of
+  // the instance runs on the same XCD -- found by exchanging XCC ids once.
+  bool plain = false;
+  {
+    unsigned xcc;
+    asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
+    xcc &= 0xFu;
+    const unsigned htag = salt | 0xFFFFFu;
+    if (tid == 0) gran_store(rs, (2u * (unsigned)a.H + (unsigned)tile) * 16u, xcc, htag, false);
+    bool ok = true;
+    if (tid < kWave) {
+      unsigned long long diff = 0ull;
+      for (int t0 = 0; t0 < a.C; t0 += kWave) {
+        unsigned long long v[1] = {xcc};
+        unsigned off[1] = {(2u * (unsigned)a.H + (unsigned)(t0 + tid)) * 16u};
+        ok &= gran_gather<1>(rs, rs, off, t0 + tid < a.C ? 1u : 0u, htag, v);
+        diff |= v[0] ^ xcc;
+      }
+      diff = wave_or_u64(diff);
+      if (tid == 0) { red[2] = diff; lflag[1] = ok ? 0 : 1; }
+    }
+    __syncthreads();
+    if (lflag[1]) { if (tid == 0) atomicOr(a.err, 1); return; }
+    plain = a.xcd_group && red[2] == 0ull;
+    __syncthreads();
+  }
 
   double* cur = bufA;
   double* oth = bufB;
   long long done = 0;  // sweeps completed before the current block
-  // phase cycle counters (thread 0): sweeps, summary + publish, barrier, refresh, blocks
+  // phase cycle counters (thread 0): sweeps, summary + publish, exchange wait, refresh, blocks
   unsigned long long st_acc[5] = {0, 0, 0, 0, 0};
   const bool stamps = a.stamps != nullptr && tid == 0;
   unsigned long long ts = stamps ? stamp_now() : 0;
@@ -259,7 +309,10 @@ __global__ void __launch_bounds__(NT) cluster_kernel(ClusterArgs a) {
     if (stamps) { const unsigned long long t = stamp_now(); st_acc[k] += t - ts; ts = t; }
   };
   auto stamp_flush = [&]() {
-    if (stamps) for (int k = 0; k < 5; ++k) a.stamps[(size_t)blockIdx.x * 8 + k] = st_acc[k];
+    if (stamps) {
+      for (int k = 0; k < 5; ++k) a.stamps[(size_t)blockIdx.x * 8 + k] = st_acc[k];
+      a.stamps[(size_t)blockIdx.x * 8 + 5] = plain ? 1 : 0;
+    }
   };
   const long long total = MODE == kModeBwd ? a.n_sweeps : -1;
   for (int m = 0;; ++m) {
@@ -274,37 +327,72 @@ __global__ void __launch_bounds__(NT) cluster_kernel(ClusterArgs a) {
     }
     stamp(0);
     if (stamps) st_acc[4] += 1;
-    // ---- per-tile summary of the block -------------------------------------
+    // ---- per-tile summary of the block (32 bits) -----------------------------
+    // forward: bit i / 16 + i = some owned |delta| > eps / NaN at sweep i;
+    // backward: scale code (common.h) of the owned maximum of the last sweep
+    unsigned* red32 = (unsigned*)red;  // [0..1]: tile summary by parity, [2..3]: instance summary
+    if (tid == 0) red32[2 + ((m + 1) & 1)] = 0u;  // last read in block m - 1
     if (MODE == kModeFwd) {
       const unsigned wf = wave_or_bits(flags, 16 + Tm) & (((1u << Tm) - 1) | (((1u << Tm) - 1) << 16));
-      if ((tid & (kWave - 1)) == 0 && wf) atomicOr((unsigned*)&red[m & 1], wf);
+      if ((tid & (kWave - 1)) == 0 && wf) atomicOr(&red32[m & 1], wf);
     } else if (a.rescale) {
-      mx = wave_max_u64(mx);
-      if ((tid & (kWave - 1)) == 0 && mx) atomicMax(&red[m & 1], mx);
+      const unsigned wc = wave_max_code(scale_code(bits_double(mx)));
+      if ((tid & (kWave - 1)) == 0 && wc) atomicMax(&red32[m & 1], wc);
     }
-    // ---- publish halo rows (write-through), combine the summaries, arrive ----
-    double* pubm = a.pub + (size_t)(m & 1) * pubStride + iS;
-    for (int l = own0 + tid; l < pubA1; l += NT) st_sc1(&pubm[base + l], cur[pad + l]);
-    for (int l = pubB0 + tid; l < own1; l += NT) st_sc1(&pubm[base + l], cur[pad + l]);
-    __syncthreads();  // the tile summary in red[m & 1] is complete
-    if (tid == 0) {
-      const unsigned long long v = red[m & 1];
-      if (MODE == kModeFwd) {
-        if (v) atomicOr(&slots[m % 3], (unsigned)v);
-      } else if (v) {
-        atomicMax(&slots64[(m % 3) + 3], v);
-      }
-      if (tile == 0) {  // the ring entry of block m + 1 was last read before barrier m - 1
-        __hip_atomic_store(&slots[(m + 1) % 3], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        __hip_atomic_store(&slots64[((m + 1) % 3) + 3], 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      }
+    // ---- publish the halo rows, tagged with the block ------------------------
+    const unsigned tag = salt | (((unsigned)m + 1u) & 0xFFFFFu);
+    const unsigned gpar = (unsigned)(m & 1) * (unsigned)S;
+    if constexpr (PAIR) {
+      unsigned pb = pub_bits;
+      asm volatile("" : "+v"(pb));  // opaque per block: keeps the slot predicates out of SGPRs
+#pragma unroll
+      for (int j = 0; j < SPT; ++j)  // per register slot: all stores of a thread in flight together
+        if ((pb >> j) & 1u)
+          gran_store(rg, (gpar + (unsigned)(base + slot_state(j))) * 16u, dbits(cv[PAIR ? j : 0]), tag, plain);
+    } else {
+      for (int l = own0 + tid; l < pubA1; l += NT)
+        gran_store(rg, (gpar + (unsigned)(base + l)) * 16u, dbits(cur[pad + l]), tag, plain);
+      for (int l = pubB0 + tid; l < own1; l += NT)
+        gran_store(rg, (gpar + (unsigned)(base + l)) * 16u, dbits(cur[pad + l]), tag, plain);
     }
+    __syncthreads();  // the tile summary in red32[m & 1] is complete
+    if (tid == 0) gran_store(rs, ((unsigned)(m & 1) * (unsigned)a.H + (unsigned)tile) * 16u, red32[m & 1], tag, plain);
     stamp(1);
-    if (!instance_barrier(&a.counter[inst], (unsigned)(a.C * (m + 1)), a.err, &lflag[0])) return;
+    // ---- gather this tile's ghost rows and (threads < C) every tile's summary,
+    // ---- all polls of a thread in flight together: one round trip --------------
+    bool ok = true;
+    constexpr int GPT = PAIR ? kGatherPerThread : 1;  // ghost granules in flight per thread
+    for (int k0 = 0; k0 < max(ng, 1); k0 += GPT * NT) {
+      unsigned off[GPT + 1];
+      int ls[GPT];
+      unsigned want = 0;
+#pragma unroll
+      for (int i = 0; i < GPT; ++i) {
+        const int k = k0 + tid + i * NT;
+        ls[i] = k < ng0 ? k : own1 + (k - ng0);
+        off[i] = (gpar + (unsigned)(base + ls[i])) * 16u;
+        want |= (k < ng ? 1u : 0u) << i;
+      }
+      off[GPT] = ((unsigned)(m & 1) * (unsigned)a.H + (unsigned)tid) * 16u;
+      want |= (k0 == 0 && tid < a.C ? 1u : 0u) << GPT;
+      unsigned long long v[GPT + 1];
+      ok &= gran_gather<GPT + 1>(rg, rs, off, want, tag, v);
+#pragma unroll
+      for (int i = 0; i < GPT; ++i)
+        if ((want >> i) & 1u) cur[pad + ls[i]] = bits_double(v[i]);
+      if ((want >> GPT) & 1u) {
+        if (MODE == kModeFwd) atomicOr(&red32[2 + (m & 1)], (unsigned)v[GPT]);
+        else atomicMax(&red32[2 + (m & 1)], (unsigned)v[GPT]);
+      }
+    }
+    if (!ok) { lflag[0] = 1; atomicOr(a.err, 1); }
+    __syncthreads();
+    if (lflag[0]) return;  // exchange timed out (reported through a.err)
+    const unsigned summary = red32[2 + (m & 1)];
+    if (tid == 0) red32[m & 1] = 0u;  // next-but-one block's tile summary (read above)
     stamp(2);
-    if (tid == 0) red[(m + 1) & 1] = 0ull;  // next block's summary word (last read above)
     if (MODE == kModeFwd) {
-      const unsigned msk = __hip_atomic_load(&slots[m % 3], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      const unsigned msk = summary;
       int conv = 0;
       bool nan_stop = false;
       for (int i = 0; i < Tm; ++i) {
@@ -334,19 +422,34 @@ __global__ void __launch_bounds__(NT) cluster_kernel(ClusterArgs a) {
       }
     }
     done += Tm;
-    // ---- refresh ghost rows from the neighbours' publications ---------------
-    int e_scale = 0;
-    if (MODE == kModeBwd && a.rescale)
-      e_scale = rescale_exponent(bits_double(
-          __hip_atomic_load(&slots64[(m % 3) + 3], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)));
-    for (int l = tid; l < E; l += NT) {
-      double v = (l >= own0 && l < own1) ? cur[pad + l] : ld_sc1(&pubm[base + l]);
-      if (MODE == kModeBwd && e_scale) v = ldexp(v, e_scale);
-      cur[pad + l] = v;
-      if (MODE == kModeFwd) snap[l] = v;
+    // ---- rescale (backward), snapshot (forward), register copy (pair) --------
+    const int e_scale = (MODE == kModeBwd && a.rescale) ? code_exponent(summary) : 0;
+    if constexpr (PAIR) {
+      unsigned ob = own_bits, xb = ext_bits;
+      asm volatile("" : "+v"(ob), "+v"(xb));
+#pragma unroll
+      for (int jp = 0; jp < SPT / 2; ++jp) {  // pairs: own / ext predicates hold for both states
+        const int l = 2 * (tid + jp * NT);
+        const bool own = (ob >> (2 * jp)) & 1u, ext = (xb >> (2 * jp)) & 1u;
+        double2 v = make_double2(cv[PAIR ? 2 * jp : 0], cv[PAIR ? 2 * jp + 1 : 0]);
+        if (!own && ext) v = *reinterpret_cast<const double2*>(cur + pad + l);  // gathered ghost pair
+        if (MODE == kModeBwd && e_scale) {
+          v.x = ldexp(v.x, e_scale);
+          v.y = ldexp(v.y, e_scale);
+          if (ext) *reinterpret_cast<double2*>(cur + pad + l) = v;
+        }
+        if (MODE == kModeFwd && ext) *reinterpret_cast<double2*>(snap + l) = v;
+        cv[PAIR ? 2 * jp : 0] = v.x;
+        cv[PAIR ? 2 * jp + 1 : 0] = v.y;
+      }
+    } else if (MODE == kModeFwd || e_scale) {
+      for (int l = tid; l < E; l += NT) {
+        double v = cur[pad + l];
+        if (MODE == kModeBwd) cur[pad + l] = v = ldexp(v, e_scale);
+        if (MODE == kModeFwd) snap[l] = v;
+      }
     }
     __syncthreads();
-    reload(cur);
     stamp(3);
     if (MODE == kModeBwd && done >= total) break;
   }
@@ -402,6 +505,8 @@ __global__ void bwd_growth_kernel(const double* __restrict__ bw, int tab_shared,
     growth[b] = mx;
   }
 }
+
+static std::atomic<unsigned> g_salt{1};  // per-launch tag salt (cluster.h granules)
 
 static int env_int(const char* name, int dflt) {
   const char* e = getenv(name);
@@ -563,6 +668,8 @@ int cluster_run(int mode, const ClusterPlan& p, ClusterArgs a, int B, hipStream_
   for (int b0 = 0; b0 < B; b0 += p.per_launch) {
     const int nb = std::min(p.per_launch, B - b0);
     a.b0 = b0;
+    a.xcd_group = (nb % 8 == 0) && env_int("IRLMX_XCD_GROUP", 1) != 0;
+    a.salt = g_salt.fetch_add(1, std::memory_order_relaxed);
     void* args[] = {&a};
     e = hipLaunchKernel(fn, dim3(nb * p.C), dim3(nt), args, p.lds, st);
     if (e != hipSuccess) return hip_fail(e, "cluster launch");
@@ -574,12 +681,12 @@ int cluster_run(int mode, const ClusterPlan& p, ClusterArgs a, int B, hipStream_
   if (stamps) {
     unsigned long long* h = (unsigned long long*)malloc(sizeof(unsigned long long) * 8 * nwg);
     hipMemcpy(h, stamps, sizeof(unsigned long long) * 8 * nwg, hipMemcpyDeviceToHost);
-    double acc[5] = {0, 0, 0, 0, 0};
+    double acc[6] = {0, 0, 0, 0, 0, 0};
     for (int g = 0; g < nwg; ++g)
-      for (int k = 0; k < 5; ++k) acc[k] += (double)h[(size_t)g * 8 + k] / nwg;
+      for (int k = 0; k < 6; ++k) acc[k] += (double)h[(size_t)g * 8 + k] / nwg;
     fprintf(stderr, "[irlmx stamps] %s%s mode=%d R=%d G=%d C=%d spt=%d blocks=%.0f  cycles/block: sweeps %.0f  publish %.0f  "
-                    "barrier %.0f  refresh %.0f\n", p.strip ? "strip" : "lds", p.pair ? "-pair" : "", mode, p.R, p.G, p.C, p.spt, acc[4], acc[0] / acc[4], acc[1] / acc[4],
-            acc[2] / acc[4], acc[3] / acc[4]);
+                    "barrier %.0f  refresh %.0f  same-xcd %.2f\n", p.strip ? "strip" : "lds", p.pair ? "-pair" : "", mode, p.R, p.G, p.C, p.spt,
+            acc[4], acc[0] / acc[4], acc[1] / acc[4], acc[2] / acc[4], acc[3] / acc[4], acc[5]);
     free(h);
     hipFree(stamps);
   }

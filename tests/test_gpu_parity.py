@@ -350,7 +350,7 @@ def test_pair_layout_bit_identical(dev, monkeypatch):
               "pair": {"IRLMX_FUSED_MAX_STATES": "0"},
               "pair_small": {"IRLMX_FUSED_MAX_STATES": "0", "IRLMX_CLUSTER_R": "7", "IRLMX_CLUSTER_G": "3"}}
     rng = np.random.default_rng(5)
-    for size, theta, cap in ((64, "ones", 20000), (64, "unif", 0), (128, "unif", 3000)):
+    for size, theta, cap in ((64, "ones", 20000), (64, "unif", 20000), (128, "unif", 3000)):
         n = size * size
         r = np.ones(n) if theta == "ones" else rng.uniform(0, 1.5, n)
         p0 = np.zeros(n)
