@@ -52,7 +52,7 @@ struct ClusterPlan {
   int R, G, C, T, per_launch, spt, emax;
   size_t lds;
   int strip, cpl, rpt;  // strip kernel (strip.hip) shape; strip == 0: LDS kernel
-  bool pair;            // LDS kernel with the pair layout (widths 64 / 128)
+  int pair;             // LDS kernel layout: 0 per state, 1 pair rows, 2 column strips (widths 64 / 128)
 };
 
 size_t strip_lds(int W, int emax, int nt);

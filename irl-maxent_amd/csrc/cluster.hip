@@ -81,9 +81,21 @@ __device__ inline double dpp_shift_f64(double x) {
   return __longlong_as_double(((long long)hi << 32) | (long long)(unsigned)lo);
 }
 
-template <int MODE, int SPT, int WT, bool PAIR, int NT>
+//
+// COLS (LAY == 2; widths 64 / 128): the pair layout turned into column
+// strips.  Lane cp of band bb (W / 2 lanes per band, NT / (W / 2) bands) holds
+// the column pair 2 cp, 2 cp + 1 of the SPT / 2 consecutive rows of its band,
+// all in registers.  Vertical neighbours are then the thread's own registers
+// except at the band's top and bottom row, which go through a small
+// double-buffered LDS boundary array -- per sweep one 16-byte write and one
+// read at each band edge instead of three 16-byte accesses per pair.
+template <int MODE, int SPT, int WT, int LAY, int NT>
 __global__ void __launch_bounds__(NT) cluster_kernel(ClusterArgs a) {
-  static_assert(!PAIR || (SPT % 2 == 0 && (WT == 64 || WT == 128)), "pair layout: even SPT, width 64/128");
+  constexpr bool PAIR = LAY >= 1, COLS = LAY == 2;
+  static_assert(!PAIR || (SPT % 2 == 0 && (WT == 64 || WT == 128)), "pair layouts: even SPT, width 64/128");
+  constexpr int RW = SPT / 2;                            // COLS: rows per band
+  constexpr int HW = WT / 2;                             // COLS: lanes per band (column pairs per row)
+  constexpr int NB = COLS ? NT / (WT ? HW : 1) : 1;      // COLS: bands
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   const int W = WT ? WT : a.W;
   const int H = a.H, S = a.S;
@@ -105,12 +117,19 @@ __global__ void __launch_bounds__(NT) cluster_kernel(ClusterArgs a) {
   const int base = e0 * W;
   const int pad = PAIR ? W : W + 1;  // pair layout keeps every pair 16-byte aligned
   const int blen = a.emax + 2 * pad;
+  const int cp = COLS ? tid % HW : 0, bb = COLS ? tid / HW : 0;  // COLS: column pair, band
   // state index of register slot j
-  auto slot_state = [&](int j) { return PAIR ? 2 * (tid + (j >> 1) * NT) + (j & 1) : tid + j * NT; };
+  auto slot_state = [&](int j) {
+    if (COLS) return (bb * RW + (j >> 1)) * W + 2 * cp + (j & 1);
+    return PAIR ? 2 * (tid + (j >> 1) * NT) + (j & 1) : tid + j * NT;
+  };
   double* bufA = (double*)smem;
-  double* bufB = bufA + blen;
+  double* bufB = bufA + (COLS ? 0 : blen);  // COLS keeps one buffer (ghost staging, final sweep)
   double* snap = bufB + blen;                                            // forward: block-start state
-  unsigned long long* red = (unsigned long long*)(snap + (MODE == kModeFwd ? a.emax : 0));  // [3]
+  // COLS: band edge rows [2 parities][NB + 2 (zero band at both ends)][2: top, bottom][HW] pairs
+  double2* bnd = (double2*)(snap + (MODE == kModeFwd ? a.emax : 0));
+  constexpr int kBndLen = COLS ? 2 * (NB + 2) * 2 * HW : 0;
+  unsigned long long* red = (unsigned long long*)(bnd + kBndLen);  // [3]
   int* lflag = (int*)(red + 3);                                          // [4]
 
   const size_t iS = (size_t)inst * S;
@@ -143,7 +162,8 @@ __global__ void __launch_bounds__(NT) cluster_kernel(ClusterArgs a) {
     for (int k = 0; k < kStencilK; ++k) asm volatile("" : "+v"(w[j][k]));
     asm volatile("" : "+v"(c0[j]));
   }
-  for (int i = tid; i < 2 * blen; i += NT) bufA[i] = 0.0;
+  for (int i = tid; i < (COLS ? 1 : 2) * blen; i += NT) bufA[i] = 0.0;
+  for (int i = tid; i < kBndLen; i += NT) bnd[i] = make_double2(0.0, 0.0);
   __syncthreads();
   for (int l = tid; l < E; l += NT) {
     double v0 = 0.0;
@@ -192,30 +212,62 @@ __global__ void __launch_bounds__(NT) cluster_kernel(ClusterArgs a) {
 
   const double eps = a.eps;
   // One Jacobi sweep over the extended tile.  Forward: sets bit i / 16 + i of
-  // `flags` for an owned |delta| > eps / NaN.  Backward: when `want_max`,
-  // returns this thread's max over owned states (for the block-end rescale).
+  // `flags` for an owned |delta| > eps / NaN.  (Backward: the owned maximum for
+  // the block-end rescale is taken once after the block's last sweep.)
   // Every slot l < SPT * NT is swept, also l >= E: those have zero weights and
   // zero c0, read only zeros (buffers are zero-filled and hold emax + 2 pads),
   // and stay 0 -- which is what state E - 1's down-neighbour must read.  No
   // per-state branch, so all LDS reads of a sweep can be in flight together.
   auto sweep = [&](const double* __restrict__ din, double* __restrict__ dout, int i, unsigned& flags,
-                   bool want_max) {
-    unsigned long long mx = 0ull;
+                   int) {
     unsigned ob = own_bits;
     asm volatile("" : "+v"(ob));  // opaque: the per-slot predicates stay a VGPR, not hoisted SGPR masks
     auto account = [&](int j, double nv, double self) {
-      if ((ob >> j) & 1u) {
-        if (MODE == kModeFwd) {
-          const double d = fabs(nv - self);
-          flags |= ((d > eps) ? 1u : 0u) << i;
-          flags |= ((d != d) ? 1u : 0u) << (16 + i);
-        } else if (want_max) {
-          const unsigned long long d = abs_bits(nv);
-          mx = d > mx ? d : mx;
-        }
+      if (MODE == kModeFwd && ((ob >> j) & 1u)) {
+        const double d = fabs(nv - self);
+        flags |= ((d > eps) ? 1u : 0u) << i;
+        flags |= ((d != d) ? 1u : 0u) << (16 + i);
       }
     };
-    if (PAIR) {
+    if constexpr (COLS) {
+      // band edge rows (old values) out, the neighbouring bands' edge rows in
+      double2* bp = bnd + (size_t)(i & 1) * (NB + 2) * 2 * HW;
+      bp[((bb + 1) * 2 + 0) * HW + cp] = make_double2(cv[0], cv[1]);
+      bp[((bb + 1) * 2 + 1) * HW + cp] = make_double2(cv[SPT - 2], cv[SPT - 1]);
+      __syncthreads();
+      double2 prev = bp[((bb + 0) * 2 + 1) * HW + cp];   // bottom row of the band above (zero band at the top)
+      const double2 below = bp[((bb + 2) * 2 + 0) * HW + cp];  // top row of the band below
+#pragma unroll
+      for (int jp = 0; jp < RW; ++jp) {
+        const double va = cv[2 * jp], vb = cv[2 * jp + 1];
+        const double2 up = prev;
+        const double2 dn = jp + 1 < RW ? make_double2(cv[COLS ? min(2 * jp + 2, SPT - 2) : 0],
+                                                      cv[COLS ? min(2 * jp + 3, SPT - 1) : 0])
+                                       : below;
+        const double lft = dpp_shift_f64<0x138>(vb);  // wave_shr1: left neighbour of state a
+        const double rgt = dpp_shift_f64<0x130>(va);  // wave_shl1: right neighbour of state b
+        const double* wa = w[2 * jp];
+        const double* wb = w[2 * jp + 1];
+        double acc = fma(wa[0], va, 0.0);
+        acc = fma(wa[1], vb, acc);
+        acc = fma(wa[2], lft, acc);
+        acc = fma(wa[3], dn.x, acc);
+        acc = fma(wa[4], up.x, acc);
+        const double na = MODE == kModeFwd ? c0[2 * jp] + acc : c0[2 * jp] * acc;
+        acc = fma(wb[0], vb, 0.0);
+        acc = fma(wb[1], rgt, acc);
+        acc = fma(wb[2], va, acc);
+        acc = fma(wb[3], dn.y, acc);
+        acc = fma(wb[4], up.y, acc);
+        const double nb = MODE == kModeFwd ? c0[2 * jp + 1] + acc : c0[2 * jp + 1] * acc;
+        account(2 * jp, na, va);
+        account(2 * jp + 1, nb, vb);
+        prev = make_double2(va, vb);
+        cv[2 * jp] = na;
+        cv[2 * jp + 1] = nb;
+      }
+      return;  // no trailing barrier: the next sweep writes the other parity
+    } else if (PAIR) {
 #pragma unroll
       for (int jp = 0; jp < SPT / 2; ++jp) {
         const int l = 2 * (tid + jp * NT);
@@ -261,7 +313,6 @@ __global__ void __launch_bounds__(NT) cluster_kernel(ClusterArgs a) {
       }
     }
     __syncthreads();
-    return mx;
   };
 
   // Halo exchange in tagged granules (cluster.h): this instance's region of
@@ -302,7 +353,7 @@ __global__ void __launch_bounds__(NT) cluster_kernel(ClusterArgs a) {
   double* oth = bufB;
   long long done = 0;  // sweeps completed before the current block
   // phase cycle counters (thread 0): sweeps, summary + publish, exchange wait, refresh, blocks
-  unsigned long long st_acc[5] = {0, 0, 0, 0, 0};
+  unsigned long long st_acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};  // [5], [6]: sub-phases of 1
   const bool stamps = a.stamps != nullptr && tid == 0;
   unsigned long long ts = stamps ? stamp_now() : 0;
   auto stamp = [&](int k) {
@@ -312,6 +363,8 @@ __global__ void __launch_bounds__(NT) cluster_kernel(ClusterArgs a) {
     if (stamps) {
       for (int k = 0; k < 5; ++k) a.stamps[(size_t)blockIdx.x * 8 + k] = st_acc[k];
       a.stamps[(size_t)blockIdx.x * 8 + 5] = plain ? 1 : 0;
+      a.stamps[(size_t)blockIdx.x * 8 + 6] = st_acc[5];
+      a.stamps[(size_t)blockIdx.x * 8 + 7] = st_acc[6];
     }
   };
   const long long total = MODE == kModeBwd ? a.n_sweeps : -1;
@@ -322,8 +375,18 @@ __global__ void __launch_bounds__(NT) cluster_kernel(ClusterArgs a) {
     unsigned flags = 0;
     unsigned long long mx = 0ull;
     for (int i = 0; i < Tm; ++i) {
-      mx = sweep(cur, oth, i, flags, i == Tm - 1);
-      double* t = cur; cur = oth; oth = t;
+      sweep(cur, oth, i, flags, 0);
+      if (!COLS) { double* t = cur; cur = oth; oth = t; }
+    }
+    if (COLS) __syncthreads();  // the last sweep's boundary reads are done
+    if (MODE == kModeBwd && a.rescale) {  // owned maximum of the block's last sweep
+      unsigned ob = own_bits;
+      asm volatile("" : "+v"(ob));
+#pragma unroll
+      for (int j = 0; j < SPT; ++j) {
+        const unsigned long long d = abs_bits(PAIR ? cv[PAIR ? j : 0] : cur[pad + slot_state(j)]);
+        if (((ob >> j) & 1u) && d > mx) mx = d;
+      }
     }
     stamp(0);
     if (stamps) st_acc[4] += 1;
@@ -339,6 +402,7 @@ __global__ void __launch_bounds__(NT) cluster_kernel(ClusterArgs a) {
       const unsigned wc = wave_max_code(scale_code(bits_double(mx)));
       if ((tid & (kWave - 1)) == 0 && wc) atomicMax(&red32[m & 1], wc);
     }
+    if (stamps) { const unsigned long long t = stamp_now(); st_acc[5] += t - ts; }
     // ---- publish the halo rows, tagged with the block ------------------------
     const unsigned tag = salt | (((unsigned)m + 1u) & 0xFFFFFu);
     const unsigned gpar = (unsigned)(m & 1) * (unsigned)S;
@@ -355,6 +419,7 @@ __global__ void __launch_bounds__(NT) cluster_kernel(ClusterArgs a) {
       for (int l = pubB0 + tid; l < own1; l += NT)
         gran_store(rg, (gpar + (unsigned)(base + l)) * 16u, dbits(cur[pad + l]), tag, plain);
     }
+    if (stamps) { const unsigned long long t = stamp_now(); st_acc[6] += t - ts; }
     __syncthreads();  // the tile summary in red32[m & 1] is complete
     if (tid == 0) gran_store(rs, ((unsigned)(m & 1) * (unsigned)a.H + (unsigned)tile) * 16u, red32[m & 1], tag, plain);
     stamp(1);
@@ -407,10 +472,18 @@ __global__ void __launch_bounds__(NT) cluster_kernel(ClusterArgs a) {
         reload(cur);
         unsigned scratch = 0;
         for (int i = 0; i < conv; ++i) {
-          sweep(cur, oth, i, scratch, false);
-          double* t = cur; cur = oth; oth = t;
+          sweep(cur, oth, i, scratch, 0);
+          if (!COLS) { double* t = cur; cur = oth; oth = t; }
         }
-        for (int l = own0 + tid; l < own1; l += NT) a.out[iS + base + l] = cur[pad + l];
+        if (COLS) {
+          unsigned ob = own_bits;
+          asm volatile("" : "+v"(ob));
+#pragma unroll
+          for (int j = 0; j < SPT; ++j)
+            if ((ob >> j) & 1u) a.out[iS + base + slot_state(j)] = cv[PAIR ? j : 0];
+        } else {
+          for (int l = own0 + tid; l < own1; l += NT) a.out[iS + base + l] = cur[pad + l];
+        }
         stamp(3);
         stamp_flush();
         if (tile == 0 && tid == 0) {
@@ -429,14 +502,14 @@ __global__ void __launch_bounds__(NT) cluster_kernel(ClusterArgs a) {
       asm volatile("" : "+v"(ob), "+v"(xb));
 #pragma unroll
       for (int jp = 0; jp < SPT / 2; ++jp) {  // pairs: own / ext predicates hold for both states
-        const int l = 2 * (tid + jp * NT);
+        const int l = slot_state(2 * jp);
         const bool own = (ob >> (2 * jp)) & 1u, ext = (xb >> (2 * jp)) & 1u;
         double2 v = make_double2(cv[PAIR ? 2 * jp : 0], cv[PAIR ? 2 * jp + 1 : 0]);
         if (!own && ext) v = *reinterpret_cast<const double2*>(cur + pad + l);  // gathered ghost pair
         if (MODE == kModeBwd && e_scale) {
           v.x = ldexp(v.x, e_scale);
           v.y = ldexp(v.y, e_scale);
-          if (ext) *reinterpret_cast<double2*>(cur + pad + l) = v;
+          if (ext && !COLS) *reinterpret_cast<double2*>(cur + pad + l) = v;
         }
         if (MODE == kModeFwd && ext) *reinterpret_cast<double2*>(snap + l) = v;
         cv[PAIR ? 2 * jp : 0] = v.x;
@@ -456,6 +529,15 @@ __global__ void __launch_bounds__(NT) cluster_kernel(ClusterArgs a) {
   stamp_flush();
 
   if (MODE == kModeBwd) {
+    if (COLS) {  // the register state into the LDS tile for the final per-action sweep
+      unsigned xb = ext_bits;
+      asm volatile("" : "+v"(xb));
+#pragma unroll
+      for (int jp = 0; jp < SPT / 2; ++jp)
+        if ((xb >> (2 * jp)) & 1u)
+          *reinterpret_cast<double2*>(cur + pad + slot_state(2 * jp)) = make_double2(cv[PAIR ? 2 * jp : 0], cv[PAIR ? 2 * jp + 1 : 0]);
+      __syncthreads();
+    }
     // last of the 2*S sweeps, per action: za = exp(r) * (P_a zs); pi = za / sum_a za
     const int A = a.A;
     const size_t tb = a.tab_shared ? 0 : (size_t)inst;
@@ -520,9 +602,12 @@ static int device_cus() {
   return cus;
 }
 
-static size_t cluster_lds(int emax, int W) {
-  // two padded ping-pong buffers + the forward's block-start snapshot + summary words
-  return 2 * (size_t)(emax + 2 * (W + 1)) * sizeof(double) + (size_t)emax * sizeof(double) + 64;
+static size_t cluster_lds(int emax, int W, int layout) {
+  // padded ping-pong buffers (one for COLS) + the forward's block-start snapshot
+  // + COLS band edge rows + summary words
+  const size_t bufs = (layout == 2 ? 1 : 2) * (size_t)(emax + 2 * (W + 1)) * sizeof(double);
+  const size_t bnd = layout == 2 ? 2 * (size_t)(kPairThreads / (W / 2) + 2) * 2 * (W / 2) * 16 : 0;
+  return bufs + (size_t)emax * sizeof(double) + bnd + 64;
 }
 
 // Tile plan for a width x height stencil grid and B instances: the fewest
@@ -533,8 +618,9 @@ bool cluster_plan(int W, int H, int B, ClusterPlan* out) {
   const int cus = device_cus();
   if (cus <= 0) return false;
   const int fR = env_int("IRLMX_CLUSTER_R", 0), fG = env_int("IRLMX_CLUSTER_G", 0);
-  // pair layout (cluster_kernel PAIR) for widths 64 / 128 unless IRLMX_PAIR=0
-  const bool pair = (W == 64 || W == 128) && env_int("IRLMX_PAIR", 1) != 0;
+  // layout for widths 64 / 128: IRLMX_PAIR = 2 (default) column strips, 1 pair rows, 0 per state
+  const int layout = (W == 64 || W == 128) ? std::max(0, std::min(2, env_int("IRLMX_PAIR", 2))) : 0;
+  const bool pair = layout > 0;
   const int nt = pair ? kPairThreads : kCT;
   const int spt_max = pair ? kSptMaxPair : kSptMax;
   const int rows_cap = nt * spt_max / W;
@@ -557,7 +643,7 @@ bool cluster_plan(int W, int H, int B, ClusterPlan* out) {
       if (cost < best - 1e-9) {
         best = cost;
         ok = true;
-        *out = ClusterPlan{R, G, C, G, std::min(per, B), spt, spt * nt, cluster_lds(spt * nt, W), 0, 0, 0, pair};
+        *out = ClusterPlan{R, G, C, G, std::min(per, B), spt, spt * nt, cluster_lds(spt * nt, W, layout), 0, 0, 0, layout};
       }
     }
   }
@@ -598,25 +684,25 @@ bool cluster_plan(int W, int H, int B, ClusterPlan* out) {
 template <int MODE, int WT>
 static void* cluster_fn_w(int spt) {
   switch (spt) {
-    case 1: return (void*)&cluster_kernel<MODE, 1, WT, false, kCT>;
-    case 2: return (void*)&cluster_kernel<MODE, 2, WT, false, kCT>;
-    case 3: return (void*)&cluster_kernel<MODE, 3, WT, false, kCT>;
-    case 4: return (void*)&cluster_kernel<MODE, 4, WT, false, kCT>;
-    case 5: return (void*)&cluster_kernel<MODE, 5, WT, false, kCT>;
-    case 6: return (void*)&cluster_kernel<MODE, 6, WT, false, kCT>;
+    case 1: return (void*)&cluster_kernel<MODE, 1, WT, 0, kCT>;
+    case 2: return (void*)&cluster_kernel<MODE, 2, WT, 0, kCT>;
+    case 3: return (void*)&cluster_kernel<MODE, 3, WT, 0, kCT>;
+    case 4: return (void*)&cluster_kernel<MODE, 4, WT, 0, kCT>;
+    case 5: return (void*)&cluster_kernel<MODE, 5, WT, 0, kCT>;
+    case 6: return (void*)&cluster_kernel<MODE, 6, WT, 0, kCT>;
   }
   return nullptr;
 }
 
-template <int MODE, int WT>
+template <int MODE, int WT, int LAY>
 static void* cluster_fn_pair(int spt) {
   switch (spt) {
-    case 2: return (void*)&cluster_kernel<MODE, 2, WT, true, kPairThreads>;
-    case 4: return (void*)&cluster_kernel<MODE, 4, WT, true, kPairThreads>;
-    case 6: return (void*)&cluster_kernel<MODE, 6, WT, true, kPairThreads>;
-    case 8: return (void*)&cluster_kernel<MODE, 8, WT, true, kPairThreads>;
-    case 10: return (void*)&cluster_kernel<MODE, 10, WT, true, kPairThreads>;
-    case 12: return (void*)&cluster_kernel<MODE, 12, WT, true, kPairThreads>;
+    case 2: return (void*)&cluster_kernel<MODE, 2, WT, LAY, kPairThreads>;
+    case 4: return (void*)&cluster_kernel<MODE, 4, WT, LAY, kPairThreads>;
+    case 6: return (void*)&cluster_kernel<MODE, 6, WT, LAY, kPairThreads>;
+    case 8: return (void*)&cluster_kernel<MODE, 8, WT, LAY, kPairThreads>;
+    case 10: return (void*)&cluster_kernel<MODE, 10, WT, LAY, kPairThreads>;
+    case 12: return (void*)&cluster_kernel<MODE, 12, WT, LAY, kPairThreads>;
   }
   return nullptr;
 }
@@ -624,10 +710,10 @@ static void* cluster_fn_pair(int spt) {
 // pair layout for widths 64 / 128 (even states per thread); compile-time LDS
 // offsets for widths 64 / 128 / 256; any other width uses WT = 0
 template <int MODE>
-static void* cluster_fn(int spt, int W, bool pair) {
-  if (pair) {
-    if (W == 64) return cluster_fn_pair<MODE, 64>(spt);
-    if (W == 128) return cluster_fn_pair<MODE, 128>(spt);
+static void* cluster_fn(int spt, int W, int layout) {
+  if (layout == 1 || layout == 2) {
+    if (W == 64) return layout == 1 ? cluster_fn_pair<MODE, 64, 1>(spt) : cluster_fn_pair<MODE, 64, 2>(spt);
+    if (W == 128) return layout == 1 ? cluster_fn_pair<MODE, 128, 1>(spt) : cluster_fn_pair<MODE, 128, 2>(spt);
     return nullptr;
   }
   switch (W) {
@@ -640,7 +726,14 @@ static void* cluster_fn(int spt, int W, bool pair) {
 
 // Launch the cluster kernel over all instances, `per_launch` at a time, then
 // check the barrier-timeout word (synchronises the stream).
-int cluster_run(int mode, const ClusterPlan& p, ClusterArgs a, int B, hipStream_t st) {
+int cluster_run(int mode, const ClusterPlan& plan, ClusterArgs a, int B, hipStream_t st) {
+  ClusterPlan p = plan;
+  if (mode == kModeFwd && p.pair == 2 && p.spt > 6) {
+    // the forward's convergence bookkeeping does not fit the column-strip kernel's
+    // registers at this depth: same tiles, pair-row layout
+    p.pair = 1;
+    p.lds = cluster_lds(p.emax, a.W, 1);
+  }
   void* fn;
   if (p.strip) fn = mode == kModeFwd ? strip_fn<kModeFwd>(p.cpl, p.rpt) : strip_fn<kModeBwd>(p.cpl, p.rpt);
   else fn = mode == kModeFwd ? cluster_fn<kModeFwd>(p.spt, a.W, p.pair) : cluster_fn<kModeBwd>(p.spt, a.W, p.pair);
@@ -681,12 +774,13 @@ int cluster_run(int mode, const ClusterPlan& p, ClusterArgs a, int B, hipStream_
   if (stamps) {
     unsigned long long* h = (unsigned long long*)malloc(sizeof(unsigned long long) * 8 * nwg);
     hipMemcpy(h, stamps, sizeof(unsigned long long) * 8 * nwg, hipMemcpyDeviceToHost);
-    double acc[6] = {0, 0, 0, 0, 0, 0};
+    double acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
     for (int g = 0; g < nwg; ++g)
-      for (int k = 0; k < 6; ++k) acc[k] += (double)h[(size_t)g * 8 + k] / nwg;
+      for (int k = 0; k < 8; ++k) acc[k] += (double)h[(size_t)g * 8 + k] / nwg;
     fprintf(stderr, "[irlmx stamps] %s%s mode=%d R=%d G=%d C=%d spt=%d blocks=%.0f  cycles/block: sweeps %.0f  publish %.0f  "
-                    "barrier %.0f  refresh %.0f  same-xcd %.2f\n", p.strip ? "strip" : "lds", p.pair ? "-pair" : "", mode, p.R, p.G, p.C, p.spt,
-            acc[4], acc[0] / acc[4], acc[1] / acc[4], acc[2] / acc[4], acc[3] / acc[4], acc[5]);
+                    "barrier %.0f  refresh %.0f  same-xcd %.2f  (publish: summary %.0f, stores %.0f)\n", p.strip ? "strip" : "lds", p.pair == 2 ? "-cols" : (p.pair == 1 ? "-pair" : ""), mode, p.R, p.G, p.C, p.spt,
+            acc[4], acc[0] / acc[4], acc[1] / acc[4], acc[2] / acc[4], acc[3] / acc[4], acc[5], acc[6] / acc[4],
+            (acc[7] - acc[6]) / acc[4]);
     free(h);
     hipFree(stamps);
   }

@@ -338,8 +338,9 @@ def test_shapes_bit_identical(dev, monkeypatch):
 
 @pytest.mark.gpu
 def test_pair_layout_bit_identical(dev, monkeypatch):
-    """The pair layout of the cluster kernel (widths 64 / 128: two states per
-    register slot, horizontal neighbours by DPP lane shifts) computes the same
+    """The pair layouts of the cluster kernel (widths 64 / 128: two states per
+    register slot, horizontal neighbours by DPP lane shifts; "rows" = pair rows
+    through LDS, default = column strips for the backward) compute the same
     float64 operations as the per-state LDS layout and the per-sweep shape, so
     policies, SVFs and sweep counts agree bit for bit -- with the planner's tiles
     and with forced small tiles (more halo exchanges, in-block rollback)."""
@@ -347,6 +348,7 @@ def test_pair_layout_bit_identical(dev, monkeypatch):
     keys = ("IRLMX_FUSED_MAX_STATES", "IRLMX_CLUSTER", "IRLMX_CLUSTER_R", "IRLMX_CLUSTER_G", "IRLMX_PAIR")
     shapes = {"sweep": {"IRLMX_FUSED_MAX_STATES": "0", "IRLMX_CLUSTER": "0"},
               "lds": {"IRLMX_FUSED_MAX_STATES": "0", "IRLMX_PAIR": "0"},
+              "rows": {"IRLMX_FUSED_MAX_STATES": "0", "IRLMX_PAIR": "1"},
               "pair": {"IRLMX_FUSED_MAX_STATES": "0"},
               "pair_small": {"IRLMX_FUSED_MAX_STATES": "0", "IRLMX_CLUSTER_R": "7", "IRLMX_CLUSTER_G": "3"}}
     rng = np.random.default_rng(5)
@@ -368,7 +370,7 @@ def test_pair_layout_bit_identical(dev, monkeypatch):
             out[name] = (pi, svf, int(k[0]))
         for k in keys:
             monkeypatch.delenv(k, raising=False)
-        for name in ("lds", "pair", "pair_small"):
+        for name in ("lds", "rows", "pair", "pair_small"):
             assert torch.equal(out["sweep"][0], out[name][0]), (size, theta, name, "pi")
             assert torch.equal(out["sweep"][1], out[name][1]), (size, theta, name, "svf")
             assert out["sweep"][2] == out[name][2], (size, theta, name)
