@@ -8,12 +8,11 @@
 
 namespace irlmx {
 
-constexpr int kCT = 1024;    // threads per cluster workgroup
-constexpr int kPairThreads = 512;  // threads per workgroup of the pair layout
-constexpr int kSptMaxPair = 12;    // states per thread of the pair layout
-constexpr int kTMax = 16;    // max sweeps per block (= max ghost rows)
-constexpr int kSptMax = 6;   // states per thread -> extended tile <= 6144 states (no VGPR spills)
-constexpr int kStripThreads = 512;  // strip kernel workgroup (2 waves per SIMD, 256 VGPRs)
+constexpr int kCT = 1024;          // threads per workgroup, per-state layout
+constexpr int kSptMax = 6;         // states per thread, per-state layout (no VGPR spills at 128 VGPRs)
+constexpr int kPairThreads = 512;  // threads per workgroup, pair layouts (256 VGPRs)
+constexpr int kSptMaxPair = 12;    // states per thread, pair layouts -> extended tile <= 6144 states
+constexpr int kTMax = 16;          // max sweeps per block (= max ghost rows)
 constexpr int kModeFwd = 0;
 constexpr int kModeBwd = 1;
 
@@ -21,7 +20,7 @@ struct ClusterArgs {
   int W, H, S, A;
   int R, G, C, T;          // rows per tile, ghost rows, tiles per instance, max sweeps per block
   int b0;                  // first instance of this launch
-  int btot;                // instances in pub / slots / counter arrays
+  int btot;                // instances in the granule arrays
   int emax;                // LDS buffer length (states)
   int tab_shared;          // backward tables shared by all instances
   const double* wgt;       // forward: [B][5][S] gather weights; backward: [B'][5][S] collapsed
@@ -34,14 +33,11 @@ struct ClusterArgs {
   long long max_iter;
   long long n_sweeps;      // backward: collapsed sweeps (2S - 1)
   int rescale;
-  double* pub;             // strip kernel: [2][B][S]
-  unsigned long long* gran;   // LDS kernel: [B][2][S] x 16-byte tagged granule pairs (halo rows)
-  unsigned long long* sgran;  // LDS kernel: [B][3][H] x 16-byte tagged granule pairs (tile summaries, XCC ids)
-  int xcd_group;           // LDS kernel: number the tiles of an instance within one XCD group
-  unsigned salt;           // LDS kernel: per-launch granule tag salt
-  unsigned long long* slots;  // [B][3][kTMax]
-  unsigned int* counter;   // [B]
-  int* err;                // [1] barrier timeout
+  unsigned long long* gran;   // [B][2][S] x 16-byte tagged granule pairs (halo rows)
+  unsigned long long* sgran;  // [B][3][H] x 16-byte tagged granule pairs (tile summaries, XCC ids)
+  int xcd_group;           // number the tiles of an instance within one XCD group
+  unsigned salt;           // per-launch granule tag salt
+  int* err;                // [1] exchange timeout
   unsigned long long* stamps;  // optional [grid][8] phase cycle counters (IRLMX_STAMPS=1), else null
   double* out;             // forward: svf [B][S]; backward: pi [B][S][A]
   int64_t* iters;
@@ -51,33 +47,16 @@ struct ClusterArgs {
 struct ClusterPlan {
   int R, G, C, T, per_launch, spt, emax;
   size_t lds;
-  int strip, cpl, rpt;  // strip kernel (strip.hip) shape; strip == 0: LDS kernel
-  int pair;             // LDS kernel layout: 0 per state, 1 pair rows, 2 column strips (widths 64 / 128)
+  int pair;             // in-tile layout: 0 per state, 1 pair rows, 2 column strips (widths 64 / 128)
 };
-
-size_t strip_lds(int W, int emax, int nt);
-template <int MODE>
-void* strip_fn(int cpl, int rpt);
-
-__device__ inline unsigned int ld_sc1(unsigned int* p) {
-  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-__device__ inline void st_sc1(double* p, double v) {  // write-through (sc1) 8-byte store
-  __hip_atomic_store((unsigned long long*)p, (unsigned long long)__double_as_longlong(v), __ATOMIC_RELAXED,
-                     __HIP_MEMORY_SCOPE_AGENT);
-}
-__device__ inline double ld_sc1(const double* p) {  // L1-bypassing (sc1) 8-byte load
-  return __longlong_as_double((long long)__hip_atomic_load((unsigned long long*)p, __ATOMIC_RELAXED,
-                                                           __HIP_MEMORY_SCOPE_AGENT));
-}
 
 // Tagged granules (cdna_hip_programming.md Guideline 16, form R2: the data is
 // the flag).  A 64-bit value v travels as one 16-byte sc1 store of
 // {lo32(v), tag, hi32(v), tag}; each 8-byte half is an untorn {value, tag}
 // granule, so a reader that sees tag == the block's epoch in both halves (sc1
 // loads: L1 bypassed, no acquire needed) holds the value of that block.  No
-// counter, no fence, one fabric round trip per exchange.  Epoch = block + 1;
-// the workspace is zeroed before every call, so no stale tag can match.
+// counter, no fence, one fabric round trip per exchange.  Tag = per-launch
+// salt | (block + 1); the workspace is also zeroed before every call.
 typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
 constexpr int kGatherPerThread = 4;
 
@@ -117,34 +96,6 @@ __device__ inline bool gran_gather(__amdgpu_buffer_rsrc_t r, __amdgpu_buffer_rsr
     __builtin_amdgcn_s_sleep(1);
   }
   return true;
-}
-
-// Arrival barrier of the C tiles of one instance, in the fence-free form of
-// MI355X_MICROARCH.md "Valid forms" (row 1): every payload byte is stored
-// write-through (sc1) and loaded with sc1 loads, every storing wave drains
-// (s_waitcnt vmcnt(0)) before the workgroup barrier, then ONE lane adds to the
-// instance's arrival counter (agent scope) and polls it with sc1 loads; the
-// other waves load after the workgroup barrier that lane joins.  Bounded by a
-// 20 s wall-clock timeout; returns false on timeout (error word set).
-__device__ inline bool instance_barrier(unsigned int* counter, unsigned int target, int* err, int* lds_flag) {
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    int abort = 0;
-    __hip_atomic_fetch_add(counter, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();  // 100 MHz
-    while (ld_sc1(counter) < target) {
-      __builtin_amdgcn_s_sleep(1);
-      if (__builtin_amdgcn_s_memrealtime() - t0 > 2000000000ull) {
-        abort = 1;
-        atomicOr(err, 1);
-        break;
-      }
-    }
-    *lds_flag = abort;
-  }
-  __syncthreads();
-  return *lds_flag == 0;
 }
 
 __device__ inline unsigned long long stamp_now() { return __builtin_amdgcn_s_memtime(); }

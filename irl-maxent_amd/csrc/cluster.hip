@@ -3,32 +3,32 @@
 // non-causal backward pass (maxent.py:119-159).
 //
 // Decomposition.  An instance's width x height grid is cut into C row tiles of
-// R rows.  Each tile is owned by one 1024-thread workgroup (one per CU, all
-// co-resident), which keeps its tile plus G ghost rows on either side in LDS
-// (two ping-pong float64 buffers) and the per-state stencil weights of that
-// extended tile in registers.  A block of T <= G sweeps runs entirely on chip:
-// after sweep i the rows that are still exact shrink by one on each ghost side,
-// so after T sweeps the owned rows are exact.  Then the tiles of an instance
-// exchange state through HBM:
+// R rows.  Each tile is owned by one workgroup (one per CU, all co-resident),
+// which keeps its tile plus G ghost rows on either side on chip (LDS and/or
+// registers, by layout -- see cluster_kernel) and the per-state stencil
+// weights of that extended tile in registers.  A block of T <= G sweeps runs
+// entirely on chip: after sweep i the rows that are still exact shrink by one
+// on each ghost side, so after T sweeps the owned rows are exact.  Then the
+// tiles of an instance exchange halos.
 //
-//   publish : every tile stores its owned rows into pub[parity][instance]
-//             (plain stores), each storing wave drains (s_waitcnt vmcnt(0)),
-//             the workgroup barriers, one lane does an agent-scope release and
-//             a relaxed agent-scope add on the instance's arrival counter;
-//   consume : that lane polls the counter (relaxed, s_sleep, bounded by a
-//             wall-clock timeout), issues one agent-scope acquire, the
-//             workgroup barriers, then plain loads of the ghost rows.
-//   (MI355X_MICROARCH.md "Workgroup dispatch ... visibility", Valid forms.)
+// Exchange (cluster.h "Tagged granules").  Every tile stores the owned rows
+// within G of its edges as {value, tag} granules (tag = call salt | block + 1)
+// plus one granule with its 32-bit block summary; every thread then polls its
+// ghost granules (and threads < C all tiles' summaries) with sc1 loads until
+// the tags match.  The data is the flag: one round trip, no counter, no fence
+// (cdna_hip_programming.md Guideline 16, R2).  Two parities of buffers: a tile
+// cannot publish block m + 2 before every tile has read block m + 1's
+// summaries, which each tile publishes only after reading block m.  Granules
+// are written through (sc1) unless all C tiles are found on one XCD (plain
+// stores then stay in that XCD's L2, where the sc1 loads are served).
 //
-// Convergence (forward).  Each tile reduces max|d_new - d_old| over its owned
-// states for every sweep of the block and max-combines it into the
-// instance's per-sweep slots (3-slot ring of blocks).  After the exchange every
-// tile reads the same slots and so takes the same decision: if the first sweep
-// with !(delta > eps) lies inside the block, every tile reloads the
-// block-start state (the previous block's publication, still intact thanks to
-// the double buffer) and re-runs exactly that many sweeps -- the same
-// arithmetic in the same order, so the result is the one the reference's loop
-// stops at.
+// Convergence (forward).  Per sweep i of a block a tile records "some owned
+// |delta| > eps" (bit i) and "some |delta| is NaN" (bit 16 + i); the OR over
+// tiles arrives with the exchange, so every tile takes the same decision: if
+// the first sweep with !(delta > eps) lies inside the block, every tile reloads
+// the block-start state (an LDS snapshot) and re-runs exactly that many sweeps
+// -- the same arithmetic in the same order, so the result is the one the
+// reference's loop stops at.
 //
 // Rescaling (backward).  The partition vector grows geometrically.  A first
 // pass bounds the per-sweep growth g of each instance; blocks are capped at
@@ -643,40 +643,9 @@ bool cluster_plan(int W, int H, int B, ClusterPlan* out) {
       if (cost < best - 1e-9) {
         best = cost;
         ok = true;
-        *out = ClusterPlan{R, G, C, G, std::min(per, B), spt, spt * nt, cluster_lds(spt * nt, W, layout), 0, 0, 0, layout};
+        *out = ClusterPlan{R, G, C, G, std::min(per, B), spt, spt * nt, cluster_lds(spt * nt, W, layout), layout};
       }
     }
-  }
-  // register-resident strip kernel (IRLMX_STRIP=1): widths 64 / 128 / 256, 512 threads, 8 bands
-  if (ok && env_int("IRLMX_STRIP", 0) && (W == 64 || W == 128 || W == 256)) {
-    const int cpl = W / 64;
-    const int nb = kStripThreads / kWave;
-    static const int rpts[] = {16, 12, 8, 6, 4, 3, 2, 1};
-    double sbest = 1e300;
-    ClusterPlan sp{};
-    bool sok = false;
-    for (int rpt : rpts) {
-      if (!strip_fn<kModeFwd>(cpl, rpt)) continue;
-      const int rows = nb * rpt;
-      for (int G = kTMax; G >= 1; --G) {
-        if (fG && G != fG) continue;
-        for (int R = std::min(H, rows - 2 * G); R >= 1; --R) {
-          if (fR && R != fR) continue;
-          const int C = (H + R - 1) / R;
-          const int per = cus / C;
-          if (per < 1) continue;
-          const int nl = (B + per - 1) / per;
-          const double cost = nl * (double)(rpt * cpl) * (G + 8.0) / G;
-          if (cost < sbest - 1e-9) {
-            sbest = cost;
-            sok = true;
-            sp = ClusterPlan{R, G, C, G, std::min(per, B), rpt * cpl, rows * W, strip_lds(W, rows * W, kStripThreads),
-                             1, cpl, rpt, false};
-          }
-        }
-      }
-    }
-    if (sok) *out = sp;
   }
   return ok;
 }
@@ -725,7 +694,7 @@ static void* cluster_fn(int spt, int W, int layout) {
 }
 
 // Launch the cluster kernel over all instances, `per_launch` at a time, then
-// check the barrier-timeout word (synchronises the stream).
+// check the exchange-timeout word (synchronises the stream).
 int cluster_run(int mode, const ClusterPlan& plan, ClusterArgs a, int B, hipStream_t st) {
   ClusterPlan p = plan;
   if (mode == kModeFwd && p.pair == 2 && p.spt > 6) {
@@ -735,9 +704,8 @@ int cluster_run(int mode, const ClusterPlan& plan, ClusterArgs a, int B, hipStre
     p.lds = cluster_lds(p.emax, a.W, 1);
   }
   void* fn;
-  if (p.strip) fn = mode == kModeFwd ? strip_fn<kModeFwd>(p.cpl, p.rpt) : strip_fn<kModeBwd>(p.cpl, p.rpt);
-  else fn = mode == kModeFwd ? cluster_fn<kModeFwd>(p.spt, a.W, p.pair) : cluster_fn<kModeBwd>(p.spt, a.W, p.pair);
-  const int nt = p.strip ? kStripThreads : (p.pair ? kPairThreads : kCT);
+  fn = mode == kModeFwd ? cluster_fn<kModeFwd>(p.spt, a.W, p.pair) : cluster_fn<kModeBwd>(p.spt, a.W, p.pair);
+  const int nt = p.pair ? kPairThreads : kCT;
   if (!fn) { set_error("cluster: no kernel for spt=%d", p.spt); return IRLMX_EINVAL; }
   hipError_t e = hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)p.lds);
   if (e != hipSuccess) return hip_fail(e, "cluster hipFuncSetAttribute");
@@ -778,13 +746,13 @@ int cluster_run(int mode, const ClusterPlan& plan, ClusterArgs a, int B, hipStre
     for (int g = 0; g < nwg; ++g)
       for (int k = 0; k < 8; ++k) acc[k] += (double)h[(size_t)g * 8 + k] / nwg;
     fprintf(stderr, "[irlmx stamps] %s%s mode=%d R=%d G=%d C=%d spt=%d blocks=%.0f  cycles/block: sweeps %.0f  publish %.0f  "
-                    "barrier %.0f  refresh %.0f  same-xcd %.2f  (publish: summary %.0f, stores %.0f)\n", p.strip ? "strip" : "lds", p.pair == 2 ? "-cols" : (p.pair == 1 ? "-pair" : ""), mode, p.R, p.G, p.C, p.spt,
+                    "wait %.0f  refresh %.0f  same-xcd %.2f  (publish: summary %.0f, stores %.0f)\n", "lds", p.pair == 2 ? "-cols" : (p.pair == 1 ? "-pair" : ""), mode, p.R, p.G, p.C, p.spt,
             acc[4], acc[0] / acc[4], acc[1] / acc[4], acc[2] / acc[4], acc[3] / acc[4], acc[5], acc[6] / acc[4],
             (acc[7] - acc[6]) / acc[4]);
     free(h);
     hipFree(stamps);
   }
-  if (err) { set_error("cluster: instance barrier timed out (workgroups not co-resident?)"); return IRLMX_EHIP; }
+  if (err) { set_error("cluster: halo exchange timed out (workgroups not co-resident?)"); return IRLMX_EHIP; }
   return 0;
 }
 

@@ -115,11 +115,8 @@ struct Ws {
   int64_t* iters;             // [B]
   int32_t* ndone;             // [1]
   // cluster shape (stencil layouts too large for one CU)
-  double* pub;                // strip kernel: [2][B][S] (aliases gran)
   unsigned long long* gran;   // [B][2][S] x 16 B
   unsigned long long* sgran;  // [B][3][H] x 16 B
-  unsigned long long* cslots; // [B][3][kTMax]
-  unsigned int* counter;      // [B]
   unsigned long long* growth; // [B]
   int* err;                   // [1]
   size_t total;
@@ -152,12 +149,9 @@ static Ws carve(const Model& m, int op, void* base) {
   w.iters = (int64_t*)take(B * sizeof(int64_t));
   w.ndone = (int32_t*)take(sizeof(int32_t) * 4);
   const bool cl = sweep && m.stencil && (op == IRLMX_OP_FORWARD || op == IRLMX_OP_BACKWARD);
-  // cluster halo exchange: [B][2][S] 16-byte granule pairs (the strip kernel's [2][B][S] doubles alias it)
+  // cluster halo exchange: [B][2][S] and [B][3][H] 16-byte granule pairs
   w.gran = (unsigned long long*)take(cl ? 2 * B * S * 16 : 0);
   w.sgran = (unsigned long long*)take(cl ? 3 * B * (size_t)m.H * 16 : 0);
-  w.pub = (double*)w.gran;
-  w.cslots = (unsigned long long*)take(cl ? B * 3 * kTMax * sizeof(unsigned long long) : 0);
-  w.counter = (unsigned int*)take(cl ? B * sizeof(unsigned int) : 0);
   w.growth = (unsigned long long*)take(cl ? B * sizeof(unsigned long long) : 0);
   w.err = (int*)take(cl ? 4 * sizeof(int) : 0);
   w.total = off;
@@ -913,7 +907,7 @@ extern "C" int irlmx_forward_svf(const irlmx_mdp* mdp, const double* p_initial, 
     ca.W = m.W; ca.H = m.H; ca.S = m.S; ca.A = m.A;
     ca.wgt = ws.wgt; ca.vin = p_initial; ca.bad = ws.bad;
     ca.eps = eps; ca.max_iter = (long long)max_iter;
-    ca.pub = ws.pub; ca.gran = ws.gran; ca.sgran = ws.sgran; ca.slots = ws.cslots; ca.counter = ws.counter; ca.err = ws.err;
+    ca.gran = ws.gran; ca.sgran = ws.sgran; ca.err = ws.err;
     ca.out = svf; ca.iters = iterations; ca.status = status;
     return cluster_run(kModeFwd, cp, ca, m.B, st);
   }
@@ -953,7 +947,7 @@ extern "C" int irlmx_backward_maxent(const irlmx_mdp* mdp, const double* reward,
     ca.tab_shared = m.shared ? 1 : 0;
     ca.wgt = ws.wgt; ca.row_val = m.row_val; ca.vin = reward; ca.term = terminal; ca.growth = ws.growth;
     ca.n_sweeps = 2LL * m.S - 1; ca.rescale = rescale;
-    ca.pub = ws.pub; ca.gran = ws.gran; ca.sgran = ws.sgran; ca.slots = ws.cslots; ca.counter = ws.counter; ca.err = ws.err;
+    ca.gran = ws.gran; ca.sgran = ws.sgran; ca.err = ws.err;
     ca.out = p_action; ca.status = status;
     return cluster_run(kModeBwd, cp, ca, m.B, st);
   }
