@@ -100,12 +100,20 @@ __device__ inline bool gran_gather(__amdgpu_buffer_rsrc_t r, __amdgpu_buffer_rsr
 
 __device__ inline unsigned long long stamp_now() { return __builtin_amdgcn_s_memtime(); }
 
-// OR of a 32-bit value over the wave (one ballot per bit that may be set).
-__device__ inline unsigned wave_or_bits(unsigned v, int nbits) {
-  unsigned out = 0;
-  for (int b = 0; b < nbits; ++b)
-    if (__ballot((v >> b) & 1u)) out |= 1u << b;
-  return out;
+// Wave-wide reduction of a 32-bit value with DPP (no LDS): butterflies inside
+// each row of 16 lanes, then row_bcast:15 / row_bcast:31 carry the row results
+// up to lane 63, whose value is returned (wave-uniform).  OP 0: max, 1: or;
+// both have identity 0.
+template <int OP>
+__device__ inline unsigned wave_reduce_u32(unsigned v) {
+  auto op = [](unsigned x, unsigned y) { return OP == 0 ? (x > y ? x : y) : (x | y); };
+  v = op(v, (unsigned)__builtin_amdgcn_update_dpp(0, (int)v, 0xB1, 0xF, 0xF, false));   // quad_perm [1,0,3,2]
+  v = op(v, (unsigned)__builtin_amdgcn_update_dpp(0, (int)v, 0x4E, 0xF, 0xF, false));   // quad_perm [2,3,0,1]
+  v = op(v, (unsigned)__builtin_amdgcn_update_dpp(0, (int)v, 0x141, 0xF, 0xF, false));  // row_half_mirror
+  v = op(v, (unsigned)__builtin_amdgcn_update_dpp(0, (int)v, 0x140, 0xF, 0xF, false));  // row_mirror
+  v = op(v, (unsigned)__builtin_amdgcn_update_dpp(0, (int)v, 0x142, 0xA, 0xF, false));  // row_bcast:15 -> rows 1, 3
+  v = op(v, (unsigned)__builtin_amdgcn_update_dpp(0, (int)v, 0x143, 0xC, 0xF, false));  // row_bcast:31 -> rows 2, 3
+  return (unsigned)__builtin_amdgcn_readlane((int)v, 63);
 }
 
 // Backward rescale summary as a 32-bit code, monotone in |m|: 0 for m == 0,
@@ -124,17 +132,6 @@ __device__ inline unsigned scale_code(double m) {
 __device__ inline int code_exponent(unsigned c) {
   return (c == 0u || c == kCodeNonFinite) ? 0 : -((int)c - (int)kCodeBias);
 }
-// max over the wave of a 13-bit code: bitwise search with ballots (no LDS)
-__device__ inline unsigned wave_max_code(unsigned c) {
-  unsigned r = 0;
-#pragma unroll
-  for (int b = 12; b >= 0; --b) {
-    const unsigned t = r | (1u << b);
-    if (__ballot(c >= t)) r = t;
-  }
-  return r;
-}
-
 __device__ inline unsigned long long wave_or_u64(unsigned long long v) {
 #pragma unroll
   for (int off = 32; off > 0; off >>= 1) v |= __shfl_xor(v, off, kWave);

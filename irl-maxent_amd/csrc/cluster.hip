@@ -235,15 +235,11 @@ __global__ void __launch_bounds__(NT) cluster_kernel(ClusterArgs a) {
       bp[((bb + 1) * 2 + 0) * HW + cp] = make_double2(cv[0], cv[1]);
       bp[((bb + 1) * 2 + 1) * HW + cp] = make_double2(cv[SPT - 2], cv[SPT - 1]);
       __syncthreads();
-      double2 prev = bp[((bb + 0) * 2 + 1) * HW + cp];   // bottom row of the band above (zero band at the top)
+      const double2 above = bp[((bb + 0) * 2 + 1) * HW + cp];  // bottom row of the band above (zero band at the top)
       const double2 below = bp[((bb + 2) * 2 + 0) * HW + cp];  // top row of the band below
-#pragma unroll
-      for (int jp = 0; jp < RW; ++jp) {
-        const double va = cv[2 * jp], vb = cv[2 * jp + 1];
-        const double2 up = prev;
-        const double2 dn = jp + 1 < RW ? make_double2(cv[COLS ? min(2 * jp + 2, SPT - 2) : 0],
-                                                      cv[COLS ? min(2 * jp + 3, SPT - 1) : 0])
-                                       : below;
+      // one row pair: old values (va, vb) of this row, up / dn = old neighbouring rows
+      auto row = [&](int jp, double2 up, double2 dn) {
+        const double va = cv[COLS ? 2 * jp : 0], vb = cv[COLS ? 2 * jp + 1 : 0];
         const double lft = dpp_shift_f64<0x138>(vb);  // wave_shr1: left neighbour of state a
         const double rgt = dpp_shift_f64<0x130>(va);  // wave_shl1: right neighbour of state b
         const double* wa = w[2 * jp];
@@ -262,9 +258,25 @@ __global__ void __launch_bounds__(NT) cluster_kernel(ClusterArgs a) {
         const double nb = MODE == kModeFwd ? c0[2 * jp + 1] + acc : c0[2 * jp + 1] * acc;
         account(2 * jp, na, va);
         account(2 * jp + 1, nb, vb);
-        prev = make_double2(va, vb);
-        cv[2 * jp] = na;
-        cv[2 * jp + 1] = nb;
+        cv[COLS ? 2 * jp : 0] = na;
+        cv[COLS ? 2 * jp + 1 : 0] = nb;
+      };
+      auto old = [&](int jp) { return make_double2(cv[COLS ? 2 * jp : 0], cv[COLS ? 2 * jp + 1 : 0]); };
+      if constexpr (RW == 1) {
+        row(0, above, below);
+      } else {
+        // interior rows first (no LDS operand: the edge reads above are still in
+        // flight), then the band's bottom and top rows
+        const double2 old0 = old(0), old1 = old(1);
+        double2 prev = old0;
+#pragma unroll
+        for (int jp = 1; jp < RW - 1; ++jp) {
+          const double2 cur_old = old(jp);
+          row(jp, prev, old(COLS ? min(jp + 1, RW - 1) : 0));
+          prev = cur_old;
+        }
+        row(RW - 1, prev, below);
+        row(0, above, old1);
       }
       return;  // no trailing barrier: the next sweep writes the other parity
     } else if (PAIR) {
@@ -390,19 +402,6 @@ __global__ void __launch_bounds__(NT) cluster_kernel(ClusterArgs a) {
     }
     stamp(0);
     if (stamps) st_acc[4] += 1;
-    // ---- per-tile summary of the block (32 bits) -----------------------------
-    // forward: bit i / 16 + i = some owned |delta| > eps / NaN at sweep i;
-    // backward: scale code (common.h) of the owned maximum of the last sweep
-    unsigned* red32 = (unsigned*)red;  // [0..1]: tile summary by parity, [2..3]: instance summary
-    if (tid == 0) red32[2 + ((m + 1) & 1)] = 0u;  // last read in block m - 1
-    if (MODE == kModeFwd) {
-      const unsigned wf = wave_or_bits(flags, 16 + Tm) & (((1u << Tm) - 1) | (((1u << Tm) - 1) << 16));
-      if ((tid & (kWave - 1)) == 0 && wf) atomicOr(&red32[m & 1], wf);
-    } else if (a.rescale) {
-      const unsigned wc = wave_max_code(scale_code(bits_double(mx)));
-      if ((tid & (kWave - 1)) == 0 && wc) atomicMax(&red32[m & 1], wc);
-    }
-    if (stamps) { const unsigned long long t = stamp_now(); st_acc[5] += t - ts; }
     // ---- publish the halo rows, tagged with the block ------------------------
     const unsigned tag = salt | (((unsigned)m + 1u) & 0xFFFFFu);
     const unsigned gpar = (unsigned)(m & 1) * (unsigned)S;
@@ -418,6 +417,19 @@ __global__ void __launch_bounds__(NT) cluster_kernel(ClusterArgs a) {
         gran_store(rg, (gpar + (unsigned)(base + l)) * 16u, dbits(cur[pad + l]), tag, plain);
       for (int l = pubB0 + tid; l < own1; l += NT)
         gran_store(rg, (gpar + (unsigned)(base + l)) * 16u, dbits(cur[pad + l]), tag, plain);
+    }
+    if (stamps) { const unsigned long long t = stamp_now(); st_acc[5] += t - ts; }
+    // ---- per-tile summary of the block (32 bits), while the halo is in flight --
+    // forward: bit i / 16 + i = some owned |delta| > eps / NaN at sweep i;
+    // backward: scale code (cluster.h) of the owned maximum of the last sweep
+    unsigned* red32 = (unsigned*)red;  // [0..1]: tile summary by parity, [2..3]: instance summary
+    if (tid == 0) red32[2 + ((m + 1) & 1)] = 0u;  // last read in block m - 1
+    if (MODE == kModeFwd) {
+      const unsigned wf = wave_reduce_u32<1>(flags) & (((1u << Tm) - 1) | (((1u << Tm) - 1) << 16));
+      if ((tid & (kWave - 1)) == 0 && wf) atomicOr(&red32[m & 1], wf);
+    } else if (a.rescale) {
+      const unsigned wc = wave_reduce_u32<0>(scale_code(bits_double(mx)));
+      if ((tid & (kWave - 1)) == 0 && wc) atomicMax(&red32[m & 1], wc);
     }
     if (stamps) { const unsigned long long t = stamp_now(); st_acc[6] += t - ts; }
     __syncthreads();  // the tile summary in red32[m & 1] is complete
@@ -746,7 +758,7 @@ int cluster_run(int mode, const ClusterPlan& plan, ClusterArgs a, int B, hipStre
     for (int g = 0; g < nwg; ++g)
       for (int k = 0; k < 8; ++k) acc[k] += (double)h[(size_t)g * 8 + k] / nwg;
     fprintf(stderr, "[irlmx stamps] %s%s mode=%d R=%d G=%d C=%d spt=%d blocks=%.0f  cycles/block: sweeps %.0f  publish %.0f  "
-                    "wait %.0f  refresh %.0f  same-xcd %.2f  (publish: summary %.0f, stores %.0f)\n", "lds", p.pair == 2 ? "-cols" : (p.pair == 1 ? "-pair" : ""), mode, p.R, p.G, p.C, p.spt,
+                    "wait %.0f  refresh %.0f  same-xcd %.2f  (publish: stores %.0f, summary %.0f)\n", "lds", p.pair == 2 ? "-cols" : (p.pair == 1 ? "-pair" : ""), mode, p.R, p.G, p.C, p.spt,
             acc[4], acc[0] / acc[4], acc[1] / acc[4], acc[2] / acc[4], acc[3] / acc[4], acc[5], acc[6] / acc[4],
             (acc[7] - acc[6]) / acc[4]);
     free(h);

@@ -158,6 +158,74 @@ def test_config1_full_irl_runs(dev):
     assert np.max(np.abs(r - z["reward_causal"])) <= 1e-9
 
 
+def test_batched_irl_config1(dev):
+    """irlmx.batch.BatchedMaxEnt run to the reference's stopping rule reproduces
+    the full config-1 irl (375 steps) and irl_causal (419 steps) rewards; two
+    instances per batch, both equal to the single reference run."""
+    from irlmx import DeviceMDP
+    from irlmx.batch import BatchedMaxEnt
+    z = load_golden("config1")
+    mdp = DeviceMDP.icy_gridworld(5, [0.2, 0.2], device=dev)
+    assert np.array_equal(mdp.select(0, 1).to_dense(), z["p_transition"])
+    e_f = np.tile(z["e_features"], (2, 1))
+    p0 = np.tile(z["p_initial"], (2, 1))
+    for causal, key, steps in ((False, "reward_maxent", "irl_steps"), (True, "reward_causal", "causal_steps")):
+        irl = BatchedMaxEnt(mdp, e_f, p0, [24], causal=causal, discount=0.7 if causal else None)
+        r, k = irl.run(eps=1e-4)
+        assert k.tolist() == [int(z[steps])] * 2, (causal, k.tolist())
+        for b in range(2):
+            assert np.max(np.abs(r[b].cpu().numpy() - z[key])) <= 1e-9, (causal, b)
+
+
+def test_batched_irl_feature_matrix(dev):
+    """Non-identity features (one-hot x and y coordinates, shared [S, F] and
+    per-instance [B, S, F]): BatchedMaxEnt.run equals the oracle's irl /
+    irl_causal loops (maxent.py:196-255, 383-453) step for step, per instance,
+    including instances that stop at different steps."""
+    from irlmx import DeviceMDP
+    from irlmx.batch import BatchedMaxEnt
+    size, n = 6, 36
+    feats = np.zeros((n, 2 * size))
+    for s in range(n):
+        feats[s, s % size] = 1.0
+        feats[s, size + s // size] = 1.0
+    slips = [0.1, 0.25, 0.4]
+    mdp = DeviceMDP.icy_gridworld(size, slips, device=dev)
+    rng = np.random.default_rng(11)
+    tjs = []
+    for b in range(3):
+        P = O.icy_gridworld_table(size, slips[b])
+        trajs = []
+        for t in range(20):
+            s, tr = int(rng.integers(0, n - 1)), []
+            for _ in range(30):
+                a = int(rng.integers(0, 4))
+                s2 = int(rng.choice(n, p=P[s, :, a]))
+                tr.append((s, a, s2))
+                s = s2
+                if s == n - 1:
+                    break
+            trajs.append(O.Trajectory(tr))
+        tjs.append(trajs)
+    e_f = np.stack([O.feature_expectation(feats, tjs[b]) for b in range(3)])
+    p0 = np.stack([O.initial_probabilities(n, tjs[b]) for b in range(3)])
+    for causal in (False, True):
+        for shared in (True, False):
+            f = feats if shared else np.tile(feats, (3, 1, 1))
+            irl = BatchedMaxEnt(mdp, e_f, p0, [n - 1], features=f, causal=causal,
+                                discount=0.7 if causal else None, rescale=False)
+            r, k = irl.run(eps=1e-4, max_steps=400)
+            for b in range(3):
+                P = O.icy_gridworld_table(size, slips[b])
+                opt = O.ExpSga(lr=O.linear_decay(0.2))
+                if causal:
+                    ref, ks = O.irl_causal(P, feats, [n - 1], tjs[b], opt, O.Constant(1.0), 0.7)
+                else:
+                    ref, ks = O.irl(P, feats, [n - 1], tjs[b], opt, O.Constant(1.0))
+                assert int(k[b]) == ks, (causal, shared, b, int(k[b]), ks)
+                close(r[b].cpu().numpy(), ref, rtol=1e-9, what=f"causal={causal} shared={shared} b={b}")
+
+
 def test_maxent_small_cases(dev, shape):
     from irlmx import DeviceMDP, ops
     z = load_golden("maxent_small")
@@ -218,6 +286,30 @@ def test_causal_small_cases(dev, shape):
     with pytest.raises(IndexError):  # as the reference (maxent.py:99) when phi reaches the forward pass
         M.compute_expected_causal_svf(O.icy_gridworld_table(5, 0.2), np.ones(25) / 25, z["phi_vec__phi"],
                                       np.ones(25), 0.8)
+
+
+def test_causal_128_config5(dev):
+    """Config 5: MaxCausalEnt soft VI on 128x128, fp64, discount
+    0.7, theta ~ U(0, 1.5) (seed 5), against the reference's own output at that size
+    (tests/golden/causal_128.npz, tools/gen_golden.py --heavy): identical sweep count,
+    max|d pi| <= 1e-9 * max|pi_ref|; then the causal forward pass runs to
+    convergence on the device policy."""
+    from irlmx import DeviceMDP, ops
+    z = load_golden("causal_128")
+    size = int(z["size"])
+    n = size * size
+    mdp = DeviceMDP.icy_gridworld(size, 0.2, device=dev)
+    pi, v, ks, st = ops.soft_backward(mdp, z["theta"], O.terminal_reward([n - 1], n), float(z["discount"]))
+    assert int(ks[0]) == int(z["k_s"]) == 812, int(ks[0])
+    got = pi[0].cpu().numpy()
+    ref = z["pi"]
+    assert np.max(np.abs(got - ref)) <= 1e-9 * np.max(np.abs(ref)), np.max(np.abs(got - ref))
+    p0 = np.zeros(n)
+    p0[0] = 1.0
+    svf, k, stf = ops.forward_svf(mdp, p0, ops.terminal_mask([n - 1], n, device=dev), pi)
+    assert int(stf[0]) == 0 and int(k[0]) > 0
+    s = svf[0].cpu().numpy()
+    assert np.all(np.isfinite(s)) and s.min() >= 0.0
 
 
 def test_value_iteration_cases(dev, shape):
