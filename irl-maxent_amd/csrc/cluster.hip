@@ -199,6 +199,21 @@ __global__ void __launch_bounds__(NT) cluster_kernel(ClusterArgs a) {
     pub_bits |= (((l >= own0 && l < pubA1) || (l >= pubB0 && l < own1)) ? 1u : 0u) << j;
   }
 
+  // Opaque per use, so the compiler does not hoist per-slot SGPR masks out of
+  // the loops (SGPR pressure).  With the pair layouts at width 128 a wave
+  // covers exactly one row per slot, so the predicates are wave-uniform: kept
+  // in an SGPR they turn into scalar branches instead of per-lane selects.
+  constexpr bool kUniformSlots = PAIR && WT == 128;
+  auto slot_bits = [&](unsigned b) {
+    if constexpr (kUniformSlots) {
+      b = (unsigned)__builtin_amdgcn_readfirstlane((int)b);
+      asm volatile("" : "+s"(b));
+    } else {
+      asm volatile("" : "+v"(b));
+    }
+    return b;
+  };
+
   int T = a.T;
   if (MODE == kModeBwd) {
     // cap the block so the growth over T sweeps stays below 2^900
@@ -220,8 +235,7 @@ __global__ void __launch_bounds__(NT) cluster_kernel(ClusterArgs a) {
   // per-state branch, so all LDS reads of a sweep can be in flight together.
   auto sweep = [&](const double* __restrict__ din, double* __restrict__ dout, int i, unsigned& flags,
                    int) {
-    unsigned ob = own_bits;
-    asm volatile("" : "+v"(ob));  // opaque: the per-slot predicates stay a VGPR, not hoisted SGPR masks
+    const unsigned ob = slot_bits(own_bits);
     auto account = [&](int j, double nv, double self) {
       if (MODE == kModeFwd && ((ob >> j) & 1u)) {
         const double d = fabs(nv - self);
@@ -244,29 +258,67 @@ __global__ void __launch_bounds__(NT) cluster_kernel(ClusterArgs a) {
         const double rgt = dpp_shift_f64<0x130>(va);  // wave_shl1: right neighbour of state b
         const double* wa = w[2 * jp];
         const double* wb = w[2 * jp + 1];
+        // the two states' chains interleaved (each in its own fixed order), so
+        // consecutive FMAs are independent
         double acc = fma(wa[0], va, 0.0);
+        double bcc = fma(wb[0], vb, 0.0);
         acc = fma(wa[1], vb, acc);
+        bcc = fma(wb[1], rgt, bcc);
         acc = fma(wa[2], lft, acc);
+        bcc = fma(wb[2], va, bcc);
         acc = fma(wa[3], dn.x, acc);
+        bcc = fma(wb[3], dn.y, bcc);
         acc = fma(wa[4], up.x, acc);
+        bcc = fma(wb[4], up.y, bcc);
         const double na = MODE == kModeFwd ? c0[2 * jp] + acc : c0[2 * jp] * acc;
-        acc = fma(wb[0], vb, 0.0);
-        acc = fma(wb[1], rgt, acc);
-        acc = fma(wb[2], va, acc);
-        acc = fma(wb[3], dn.y, acc);
-        acc = fma(wb[4], up.y, acc);
-        const double nb = MODE == kModeFwd ? c0[2 * jp + 1] + acc : c0[2 * jp + 1] * acc;
+        const double nb = MODE == kModeFwd ? c0[2 * jp + 1] + bcc : c0[2 * jp + 1] * bcc;
         account(2 * jp, na, va);
         account(2 * jp + 1, nb, vb);
         cv[COLS ? 2 * jp : 0] = na;
         cv[COLS ? 2 * jp + 1 : 0] = nb;
       };
       auto old = [&](int jp) { return make_double2(cv[COLS ? 2 * jp : 0], cv[COLS ? 2 * jp + 1 : 0]); };
+      // two row pairs at once: four independent FMA chains interleaved
+      auto row2 = [&](int j1, double2 up1, double2 dn1, int j2, double2 up2, double2 dn2) {
+        const double a1 = cv[COLS ? 2 * j1 : 0], b1 = cv[COLS ? 2 * j1 + 1 : 0];
+        const double a2 = cv[COLS ? 2 * j2 : 0], b2 = cv[COLS ? 2 * j2 + 1 : 0];
+        const double l1 = dpp_shift_f64<0x138>(b1), r1 = dpp_shift_f64<0x130>(a1);
+        const double l2 = dpp_shift_f64<0x138>(b2), r2 = dpp_shift_f64<0x130>(a2);
+        const double *wa1 = w[2 * j1], *wb1 = w[2 * j1 + 1], *wa2 = w[2 * j2], *wb2 = w[2 * j2 + 1];
+        double p = fma(wa1[0], a1, 0.0), q = fma(wb1[0], b1, 0.0);
+        double u = fma(wa2[0], a2, 0.0), x = fma(wb2[0], b2, 0.0);
+        p = fma(wa1[1], b1, p);   q = fma(wb1[1], r1, q);   u = fma(wa2[1], b2, u);   x = fma(wb2[1], r2, x);
+        p = fma(wa1[2], l1, p);   q = fma(wb1[2], a1, q);   u = fma(wa2[2], l2, u);   x = fma(wb2[2], a2, x);
+        p = fma(wa1[3], dn1.x, p); q = fma(wb1[3], dn1.y, q); u = fma(wa2[3], dn2.x, u); x = fma(wb2[3], dn2.y, x);
+        p = fma(wa1[4], up1.x, p); q = fma(wb1[4], up1.y, q); u = fma(wa2[4], up2.x, u); x = fma(wb2[4], up2.y, x);
+        const double n1a = MODE == kModeFwd ? c0[2 * j1] + p : c0[2 * j1] * p;
+        const double n1b = MODE == kModeFwd ? c0[2 * j1 + 1] + q : c0[2 * j1 + 1] * q;
+        const double n2a = MODE == kModeFwd ? c0[2 * j2] + u : c0[2 * j2] * u;
+        const double n2b = MODE == kModeFwd ? c0[2 * j2 + 1] + x : c0[2 * j2 + 1] * x;
+        account(2 * j1, n1a, a1);
+        account(2 * j1 + 1, n1b, b1);
+        account(2 * j2, n2a, a2);
+        account(2 * j2 + 1, n2b, b2);
+        cv[COLS ? 2 * j1 : 0] = n1a;
+        cv[COLS ? 2 * j1 + 1 : 0] = n1b;
+        cv[COLS ? 2 * j2 : 0] = n2a;
+        cv[COLS ? 2 * j2 + 1 : 0] = n2b;
+      };
       if constexpr (RW == 1) {
         row(0, above, below);
+      } else if constexpr (RW >= 4 && RW % 2 == 0) {
+        // interior rows two at a time (no LDS operand: the edge reads above are
+        // still in flight), then the band's bottom and top rows together
+        const double2 old1 = old(1);
+        double2 prev = old(0);
+#pragma unroll
+        for (int jp = 1; jp + 1 < RW - 1; jp += 2) {
+          const double2 o1 = old(jp + 1);
+          row2(jp, prev, o1, jp + 1, old(jp), old(COLS ? min(jp + 2, RW - 1) : 0));
+          prev = o1;
+        }
+        row2(RW - 1, prev, below, 0, above, old1);
       } else {
-        // interior rows first (no LDS operand: the edge reads above are still in
-        // flight), then the band's bottom and top rows
         const double2 old0 = old(0), old1 = old(1);
         double2 prev = old0;
 #pragma unroll
@@ -392,8 +444,7 @@ __global__ void __launch_bounds__(NT) cluster_kernel(ClusterArgs a) {
     }
     if (COLS) __syncthreads();  // the last sweep's boundary reads are done
     if (MODE == kModeBwd && a.rescale) {  // owned maximum of the block's last sweep
-      unsigned ob = own_bits;
-      asm volatile("" : "+v"(ob));
+      const unsigned ob = slot_bits(own_bits);
 #pragma unroll
       for (int j = 0; j < SPT; ++j) {
         const unsigned long long d = abs_bits(PAIR ? cv[PAIR ? j : 0] : cur[pad + slot_state(j)]);
@@ -406,8 +457,7 @@ __global__ void __launch_bounds__(NT) cluster_kernel(ClusterArgs a) {
     const unsigned tag = salt | (((unsigned)m + 1u) & 0xFFFFFu);
     const unsigned gpar = (unsigned)(m & 1) * (unsigned)S;
     if constexpr (PAIR) {
-      unsigned pb = pub_bits;
-      asm volatile("" : "+v"(pb));  // opaque per block: keeps the slot predicates out of SGPRs
+      const unsigned pb = slot_bits(pub_bits);
 #pragma unroll
       for (int j = 0; j < SPT; ++j)  // per register slot: all stores of a thread in flight together
         if ((pb >> j) & 1u)
@@ -488,8 +538,7 @@ __global__ void __launch_bounds__(NT) cluster_kernel(ClusterArgs a) {
           if (!COLS) { double* t = cur; cur = oth; oth = t; }
         }
         if (COLS) {
-          unsigned ob = own_bits;
-          asm volatile("" : "+v"(ob));
+          const unsigned ob = slot_bits(own_bits);
 #pragma unroll
           for (int j = 0; j < SPT; ++j)
             if ((ob >> j) & 1u) a.out[iS + base + slot_state(j)] = cv[PAIR ? j : 0];
@@ -510,8 +559,7 @@ __global__ void __launch_bounds__(NT) cluster_kernel(ClusterArgs a) {
     // ---- rescale (backward), snapshot (forward), register copy (pair) --------
     const int e_scale = (MODE == kModeBwd && a.rescale) ? code_exponent(summary) : 0;
     if constexpr (PAIR) {
-      unsigned ob = own_bits, xb = ext_bits;
-      asm volatile("" : "+v"(ob), "+v"(xb));
+      const unsigned ob = slot_bits(own_bits), xb = slot_bits(ext_bits);
 #pragma unroll
       for (int jp = 0; jp < SPT / 2; ++jp) {  // pairs: own / ext predicates hold for both states
         const int l = slot_state(2 * jp);
@@ -542,8 +590,7 @@ __global__ void __launch_bounds__(NT) cluster_kernel(ClusterArgs a) {
 
   if (MODE == kModeBwd) {
     if (COLS) {  // the register state into the LDS tile for the final per-action sweep
-      unsigned xb = ext_bits;
-      asm volatile("" : "+v"(xb));
+      const unsigned xb = slot_bits(ext_bits);
 #pragma unroll
       for (int jp = 0; jp < SPT / 2; ++jp)
         if ((xb >> (2 * jp)) & 1u)
