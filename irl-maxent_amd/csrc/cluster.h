@@ -23,7 +23,7 @@ struct ClusterArgs {
   int btot;                // instances in the granule arrays
   int emax;                // LDS buffer length (states)
   int tab_shared;          // backward tables shared by all instances
-  const double* wgt;       // forward: [B][5][S] gather weights; backward: [B'][5][S] collapsed
+  const double* wgt;       // forward: [B][5][S] gather weights; backward: [B][5][S] collapsed, reward-folded
   const double* row_val;   // backward final sweep: [B'][A][5][S]
   const double* vin;       // forward: p0 [B][S]; backward: reward [B][S]
   const uint8_t* term;     // backward: terminal mask [B][S]
@@ -140,7 +140,6 @@ __device__ inline unsigned long long wave_or_u64(unsigned long long v) {
 
 bool cluster_plan(int W, int H, int B, ClusterPlan* out);
 int cluster_run(int mode, const ClusterPlan& p, ClusterArgs a, int B, hipStream_t st);
-__global__ void bwd_growth_kernel(const double* __restrict__ bw, int tab_shared, const double* __restrict__ reward,
-                                  int S, unsigned long long* __restrict__ growth);
+__global__ void bwd_growth_kernel(const double* __restrict__ bw, int S, unsigned long long* __restrict__ growth);
 
 }  // namespace irlmx

@@ -141,18 +141,18 @@ __global__ void __launch_bounds__(NT) cluster_kernel(ClusterArgs a) {
   }
 
   // ---- per-state constants into registers --------------------------------
-  double w[SPT][kStencilK];
-  double c0[SPT];  // forward: p0; backward: exp(r), applied after the row sum as in the other shapes
-  const size_t wbase = (MODE == kModeBwd && a.tab_shared) ? 0 : iS * kStencilK;
+  double w[SPT][kStencilK];     // forward: gather weights; backward: reward-folded weights
+  double c0[MODE == kModeFwd ? SPT : 1];  // forward: p0
+  const size_t wbase = iS * kStencilK;
 #pragma unroll
   for (int j = 0; j < SPT; ++j) {
     const int l = slot_state(j);
-    c0[j] = 0.0;
+    if (MODE == kModeFwd) c0[MODE == kModeFwd ? j : 0] = 0.0;
 #pragma unroll
     for (int k = 0; k < kStencilK; ++k) w[j][k] = 0.0;
     if (l < E) {
       const int s = base + l;
-      c0[j] = MODE == kModeFwd ? a.vin[iS + s] : exp(a.vin[iS + s]);
+      if (MODE == kModeFwd) c0[MODE == kModeFwd ? j : 0] = a.vin[iS + s];
 #pragma unroll
       for (int k = 0; k < kStencilK; ++k) w[j][k] = a.wgt[wbase + (size_t)k * S + s];
     }
@@ -160,8 +160,10 @@ __global__ void __launch_bounds__(NT) cluster_kernel(ClusterArgs a) {
     // from global memory inside every sweep (rematerialisation of invariant loads)
 #pragma unroll
     for (int k = 0; k < kStencilK; ++k) asm volatile("" : "+v"(w[j][k]));
-    asm volatile("" : "+v"(c0[j]));
+    if (MODE == kModeFwd) asm volatile("" : "+v"(c0[MODE == kModeFwd ? j : 0]));
   }
+  // one sweep's new value from the weighted sum: forward p0 + sum, backward the sum
+  auto finish = [&](int j, double acc) { return MODE == kModeFwd ? c0[MODE == kModeFwd ? j : 0] + acc : acc; };
   for (int i = tid; i < (COLS ? 1 : 2) * blen; i += NT) bufA[i] = 0.0;
   for (int i = tid; i < kBndLen; i += NT) bnd[i] = make_double2(0.0, 0.0);
   __syncthreads();
@@ -270,8 +272,8 @@ __global__ void __launch_bounds__(NT) cluster_kernel(ClusterArgs a) {
         bcc = fma(wb[3], dn.y, bcc);
         acc = fma(wa[4], up.x, acc);
         bcc = fma(wb[4], up.y, bcc);
-        const double na = MODE == kModeFwd ? c0[2 * jp] + acc : c0[2 * jp] * acc;
-        const double nb = MODE == kModeFwd ? c0[2 * jp + 1] + bcc : c0[2 * jp + 1] * bcc;
+        const double na = finish(2 * jp, acc);
+        const double nb = finish(2 * jp + 1, bcc);
         account(2 * jp, na, va);
         account(2 * jp + 1, nb, vb);
         cv[COLS ? 2 * jp : 0] = na;
@@ -291,10 +293,8 @@ __global__ void __launch_bounds__(NT) cluster_kernel(ClusterArgs a) {
         p = fma(wa1[2], l1, p);   q = fma(wb1[2], a1, q);   u = fma(wa2[2], l2, u);   x = fma(wb2[2], a2, x);
         p = fma(wa1[3], dn1.x, p); q = fma(wb1[3], dn1.y, q); u = fma(wa2[3], dn2.x, u); x = fma(wb2[3], dn2.y, x);
         p = fma(wa1[4], up1.x, p); q = fma(wb1[4], up1.y, q); u = fma(wa2[4], up2.x, u); x = fma(wb2[4], up2.y, x);
-        const double n1a = MODE == kModeFwd ? c0[2 * j1] + p : c0[2 * j1] * p;
-        const double n1b = MODE == kModeFwd ? c0[2 * j1 + 1] + q : c0[2 * j1 + 1] * q;
-        const double n2a = MODE == kModeFwd ? c0[2 * j2] + u : c0[2 * j2] * u;
-        const double n2b = MODE == kModeFwd ? c0[2 * j2 + 1] + x : c0[2 * j2 + 1] * x;
+        const double n1a = finish(2 * j1, p), n1b = finish(2 * j1 + 1, q);
+        const double n2a = finish(2 * j2, u), n2b = finish(2 * j2 + 1, x);
         account(2 * j1, n1a, a1);
         account(2 * j1 + 1, n1b, b1);
         account(2 * j2, n2a, a2);
@@ -347,13 +347,13 @@ __global__ void __launch_bounds__(NT) cluster_kernel(ClusterArgs a) {
         acc = fma(wa[2], lft, acc);
         acc = fma(wa[3], dn.x, acc);
         acc = fma(wa[4], up.x, acc);
-        const double na = MODE == kModeFwd ? c0[2 * jp] + acc : c0[2 * jp] * acc;
+        const double na = finish(2 * jp, acc);
         acc = fma(wb[0], vb, 0.0);
         acc = fma(wb[1], rgt, acc);
         acc = fma(wb[2], va, acc);
         acc = fma(wb[3], dn.y, acc);
         acc = fma(wb[4], up.y, acc);
-        const double nb = MODE == kModeFwd ? c0[2 * jp + 1] + acc : c0[2 * jp + 1] * acc;
+        const double nb = finish(2 * jp + 1, acc);
         *reinterpret_cast<double2*>(dout + W + l) = make_double2(na, nb);
         account(2 * jp, na, va);
         account(2 * jp + 1, nb, vb);
@@ -371,7 +371,7 @@ __global__ void __launch_bounds__(NT) cluster_kernel(ClusterArgs a) {
         acc = fma(w[j][2], q[W - 1], acc);
         acc = fma(w[j][3], q[2 * W], acc);
         acc = fma(w[j][4], q[0], acc);
-        const double nv = MODE == kModeFwd ? c0[j] + acc : c0[j] * acc;
+        const double nv = finish(j, acc);
         dout[pad + l] = nv;
         account(j, nv, self);
       }
@@ -626,16 +626,16 @@ __global__ void __launch_bounds__(NT) cluster_kernel(ClusterArgs a) {
 
 namespace irlmx {
 
-// Per-instance bound on the backward's per-sweep growth: max_s exp(r_s) * sum_k bw[k][s].
-__global__ void bwd_growth_kernel(const double* __restrict__ bw, int tab_shared, const double* __restrict__ reward,
-                                  int S, unsigned long long* __restrict__ growth) {
+// Per-instance bound on the backward's per-sweep growth: max_s sum_k bw[b][k][s]
+// (reward-folded weights, fixed_point.hip bwd_weights_kernel).
+__global__ void bwd_growth_kernel(const double* __restrict__ bw, int S, unsigned long long* __restrict__ growth) {
   const int b = blockIdx.x;
-  const double* wb = bw + (tab_shared ? 0 : (size_t)b * kStencilK * S);
+  const double* wb = bw + (size_t)b * kStencilK * S;
   unsigned long long mx = 0ull;
   for (int s = threadIdx.x; s < S; s += blockDim.x) {
     double row = 0.0;
     for (int k = 0; k < kStencilK; ++k) row += wb[(size_t)k * S + s];
-    mx = max(mx, abs_bits(exp(reward[(size_t)b * S + s]) * row));
+    mx = max(mx, abs_bits(row));
   }
   __shared__ unsigned long long red[16];
   mx = wave_max_u64(mx);

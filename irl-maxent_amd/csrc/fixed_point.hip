@@ -106,7 +106,7 @@ __device__ inline int col_src(const Model& m, int b, int t, int k) {
 // ---------------------------------------------------------------------------
 
 struct Ws {
-  double* wgt;                // forward: [B][Kc][S] gather weights; backward: [B'][K][S]
+  double* wgt;                // forward: [B][Kc][S] gather weights; backward: [B][K][S] reward-folded
   int32_t* bad;               // [B] forward: policy has a non-finite entry
   double* buf0;               // [B][S]   sweep path ping
   double* buf1;               // [B][S]   sweep path pong
@@ -138,7 +138,7 @@ static Ws carve(const Model& m, int op, void* base) {
   const size_t B = m.B, S = m.S;
   size_t nw = 0;
   if (op == IRLMX_OP_FORWARD) nw = B * m.Kc * S;
-  if (op == IRLMX_OP_BACKWARD) nw = (m.shared ? 1 : B) * m.K * S;
+  if (op == IRLMX_OP_BACKWARD) nw = B * m.K * S;  // reward-folded: one set per instance
   w.wgt = (double*)take(nw * sizeof(double));
   w.bad = (int32_t*)take(B * sizeof(int32_t));
   const bool sweep = !use_fused(m, op);
@@ -200,16 +200,23 @@ __global__ void fwd_weights_kernel(Model m, const double* __restrict__ pi,
   if (nonfinite) atomicOr(&bad[b], 1);
 }
 
-// Collapsed backward weights: sum_a P[s, target_k(s), a] (reward independent).
-__global__ void bwd_weights_kernel(Model m, double* __restrict__ w) {
+// Collapsed, reward-folded backward weights of instance b:
+//   w[b][k][s] = exp(r[b][s]) * sum_a P[s, target_k(s), a]
+// so one backward sweep is zs'[s] = sum_k w[b][k][s] * zs[target_k(s)]
+// (maxent.py:155-156 with the action sum and exp(r) taken out of the loop).
+// Every shape (fused, sweep, cluster) uses these same weights in the same
+// order, so the shapes stay bit-identical to each other.
+__global__ void bwd_weights_kernel(Model m, const double* __restrict__ reward, double* __restrict__ w) {
   const int s = blockIdx.x * blockDim.x + threadIdx.x;
-  const int bi = blockIdx.y;  // table instance
+  const int b = blockIdx.y;
   if (s >= m.S) return;
+  const size_t bi = m.shared ? 0 : (size_t)b;  // table instance
+  const double er = exp(reward[(size_t)b * m.S + s]);
   for (int k = 0; k < m.K; ++k) {
     double acc = 0.0;
     for (int a = 0; a < m.A; ++a)
-      acc += m.row_val[(((size_t)bi * m.A + a) * m.K + k) * m.S + s];
-    w[((size_t)bi * m.K + k) * m.S + s] = acc;
+      acc += m.row_val[((bi * m.A + a) * m.K + k) * m.S + s];
+    w[((size_t)b * m.K + k) * m.S + s] = __dmul_rn(er, acc);
   }
 }
 
@@ -315,7 +322,7 @@ __global__ void __launch_bounds__(1024) fwd_fused_kernel(FwdArgs a) {
 
 struct BwdArgs {
   Model m;
-  const double* w;  // [B'][K][S] collapsed weights
+  const double* w;  // [B][K][S] collapsed, reward-folded weights
   const double* reward;
   const uint8_t* term;
   int rescale;
@@ -335,16 +342,13 @@ __global__ void __launch_bounds__(1024) bwd_fused_kernel(BwdArgs a) {
 
   double w[SPT][KMAX];
   int nb[SPT][KMAX];
-  double er[SPT];
-  const double* wb = a.w + inst_of(m, b) * K * S;
+  const double* wb = a.w + (size_t)b * K * S;
 #pragma unroll
   for (int j = 0; j < SPT; ++j) {
     const int s = tid + j * nt;
-    er[j] = 0.0;
 #pragma unroll
     for (int k = 0; k < KMAX; ++k) { w[j][k] = 0.0; nb[j][k] = 0; }
     if (s < S) {
-      er[j] = exp(a.reward[(size_t)b * S + s]);
 #pragma unroll
       for (int k = 0; k < KMAX; ++k)
         if (k < K) { w[j][k] = wb[(size_t)k * S + s]; nb[j][k] = row_nbr(m, b, s, k); }
@@ -371,7 +375,7 @@ __global__ void __launch_bounds__(1024) bwd_fused_kernel(BwdArgs a) {
 #pragma unroll
         for (int k = 0; k < KMAX; ++k)
           if (k < K) acc = fma(w[j][k], din[nb[j][k]], acc);
-        const double nv = ldexp(__dmul_rn(er[j], acc), e);
+        const double nv = ldexp(acc, e);
         dout[s] = nv;
         const unsigned long long d = abs_bits(nv);
         mx = d > mx ? d : mx;
@@ -391,6 +395,7 @@ __global__ void __launch_bounds__(1024) bwd_fused_kernel(BwdArgs a) {
   for (int j = 0; j < SPT; ++j) {
     const int s = tid + j * nt;
     if (s < S) {
+      const double er = exp(a.reward[(size_t)b * S + s]);
       double za[kMaxActions];
       double zsum = 0.0;
       for (int act = 0; act < A; ++act) {
@@ -398,7 +403,7 @@ __global__ void __launch_bounds__(1024) bwd_fused_kernel(BwdArgs a) {
 #pragma unroll
         for (int k = 0; k < KMAX; ++k)
           if (k < K) acc = fma(row_val(m, b, act, k, s), zs[nb[j][k]], acc);
-        za[act] = ldexp(__dmul_rn(er[j], acc), e);  // rounded product, then the sum (maxent.py:155-156)
+        za[act] = ldexp(__dmul_rn(er, acc), e);  // rounded product, then the sum (maxent.py:155-156)
         zsum = __dadd_rn(zsum, za[act]);
       }
       for (int act = 0; act < A; ++act) a.pi[((size_t)b * S + s) * A + act] = za[act] / zsum;
@@ -644,10 +649,10 @@ bwd_sweep_kernel(BwdArgs a, Ws ws, long long it, int r3) {
   if (a.rescale && it > 0) e = rescale_exponent(bits_double(ws.slots[b * 3 + (r3 == 0 ? 2 : r3 - 1)]));
   unsigned long long d = 0ull;
   if (s < S) {
-    const double* wb = a.w + inst_of(m, b) * m.K * S;
+    const double* wb = a.w + (size_t)b * m.K * S;
     double acc = 0.0;
     for (int k = 0; k < m.K; ++k) acc = fma(wb[(size_t)k * S + s], din[row_nbr(m, b, s, k)], acc);
-    const double nv = ldexp(__dmul_rn(exp(a.reward[(size_t)b * S + s]), acc), e);
+    const double nv = ldexp(acc, e);
     dout[s] = nv;
     d = abs_bits(nv);
   }
@@ -931,7 +936,7 @@ extern "C" int irlmx_backward_maxent(const irlmx_mdp* mdp, const double* reward,
   Ws ws = carve(m, IRLMX_OP_BACKWARD, workspace);
   hipError_t e = hipMemsetAsync(workspace, 0, ws.total, st);
   if (e != hipSuccess) return hip_fail(e, "workspace memset");
-  hipLaunchKernelGGL(bwd_weights_kernel, dim3((m.S + 255) / 256, m.shared ? 1 : m.B), dim3(256), 0, st, m, ws.wgt);
+  hipLaunchKernelGGL(bwd_weights_kernel, dim3((m.S + 255) / 256, m.B), dim3(256), 0, st, m, reward, ws.wgt);
   BwdArgs a{m, ws.wgt, reward, terminal, rescale, p_action, status};
   FusedShape fs;
   if (fused_shape(m, IRLMX_OP_BACKWARD, &fs)) {
@@ -940,8 +945,7 @@ extern "C" int irlmx_backward_maxent(const irlmx_mdp* mdp, const double* reward,
   }
   ClusterPlan cp;
   if (m.stencil && m.A <= kMaxActions && cluster_plan(m.W, m.H, m.B, &cp)) {
-    hipLaunchKernelGGL(bwd_growth_kernel, dim3(m.B), dim3(1024), 0, st, ws.wgt, m.shared ? 1 : 0, reward, m.S,
-                       ws.growth);
+    hipLaunchKernelGGL(bwd_growth_kernel, dim3(m.B), dim3(1024), 0, st, ws.wgt, m.S, ws.growth);
     ClusterArgs ca{};
     ca.W = m.W; ca.H = m.H; ca.S = m.S; ca.A = m.A;
     ca.tab_shared = m.shared ? 1 : 0;

@@ -244,8 +244,10 @@ def test_maxent_small_cases(dev, shape):
             svf, k, st = ops.forward_svf(mdp, z[c + "__p0"], tm, pi)
             kr = int(z[c + "__k_f"])
             # s8_unif mixes so slowly (11.9M sweeps, spectral radius ~1 - 1e-6) that
-            # delta crosses eps within rounding of the last few sweeps: +-1 allowed there
-            slack = 1 if kr > 1_000_000 else 0
+            # the sweep at which delta crosses eps moves with the last bits of pi
+            # (the backward's summation order differs from numpy's dgemv): a relative
+            # 1e-6 (12 sweeps) is allowed there; the SVF itself is checked below
+            slack = int(kr * 1e-6) if kr > 1_000_000 else 0
             assert abs(int(k[0]) - kr) <= slack, (c, int(k[0]), kr)
             close(svf[0].cpu().numpy(), z[c + "__svf"], rtol=1e-8, what=c + " svf")
         else:
