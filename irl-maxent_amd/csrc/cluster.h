@@ -20,6 +20,7 @@ struct ClusterArgs {
   int W, H, S, A;
   int R, G, C, T;          // rows per tile, ghost rows, tiles per instance, max sweeps per block
   int b0;                  // first instance of this launch
+  int nb;                  // instances in this launch
   int btot;                // instances in the granule arrays
   int emax;                // LDS buffer length (states)
   int tab_shared;          // backward tables shared by all instances

@@ -100,11 +100,18 @@ __global__ void __launch_bounds__(NT) cluster_kernel(ClusterArgs a) {
   const int W = WT ? WT : a.W;
   const int H = a.H, S = a.S;
   // XCD-grouped numbering (a.xcd_group): workgroups are dealt round-robin over
-  // the 8 XCDs, so blockIdx % 8 names an XCD group; the C tiles of an instance
-  // are taken from one group, which lets their halo hand-offs stay inside one
-  // L2 when the dealing is as observed (verified at run time below; speed only)
-  int lin = blockIdx.x;
-  if (a.xcd_group) lin = (blockIdx.x % 8) * (gridDim.x / 8) + blockIdx.x / 8;
+  // the 8 XCDs, so blockIdx % 8 names an XCD group; all C tiles of an instance
+  // are taken from one group (instance g + 8 j of group g), which lets their
+  // halo hand-offs stay inside one L2 when the dealing is as observed (checked
+  // at run time below; speed only).  The grid is padded to 8 equal groups; the
+  // padding workgroups leave at once.
+  int lin = blockIdx.x;  // = local instance * C + tile
+  if (a.xcd_group) {
+    const int g = blockIdx.x % 8, k = blockIdx.x / 8;
+    const int il = g + 8 * (k / a.C);
+    if (il >= a.nb) return;
+    lin = il * a.C + k % a.C;
+  }
   const int tile = lin % a.C;
   const int inst = a.b0 + lin / a.C;
   const int tid = threadIdx.x;
@@ -425,10 +432,10 @@ __global__ void __launch_bounds__(NT) cluster_kernel(ClusterArgs a) {
   };
   auto stamp_flush = [&]() {
     if (stamps) {
-      for (int k = 0; k < 5; ++k) a.stamps[(size_t)blockIdx.x * 8 + k] = st_acc[k];
-      a.stamps[(size_t)blockIdx.x * 8 + 5] = plain ? 1 : 0;
-      a.stamps[(size_t)blockIdx.x * 8 + 6] = st_acc[5];
-      a.stamps[(size_t)blockIdx.x * 8 + 7] = st_acc[6];
+      for (int k = 0; k < 5; ++k) a.stamps[(size_t)lin * 8 + k] = st_acc[k];
+      a.stamps[(size_t)lin * 8 + 5] = plain ? 1 : 0;
+      a.stamps[(size_t)lin * 8 + 6] = st_acc[5];
+      a.stamps[(size_t)lin * 8 + 7] = st_acc[6];
     }
   };
   const long long total = MODE == kModeBwd ? a.n_sweeps : -1;
@@ -661,6 +668,13 @@ static int device_cus() {
   return cus;
 }
 
+// Can the C tiles of each of nb instances sit in one XCD group (<= CUs / 8
+// workgroups per group, one per CU)?
+static bool xcd_groupable(int nb, int C) {
+  const int cus = device_cus();
+  return cus >= 8 && ((nb + 7) / 8) * C <= cus / 8;
+}
+
 static size_t cluster_lds(int emax, int W, int layout) {
   // padded ping-pong buffers (one for COLS) + the forward's block-start snapshot
   // + COLS band edge rows + summary words
@@ -698,7 +712,11 @@ bool cluster_plan(int W, int H, int B, ClusterPlan* out) {
       const int per = cus / C;
       if (per < 1) continue;
       const int nl = (B + per - 1) / per;
-      const double cost = nl * (double)spt * (G + 8.0) / G;
+      // cycles per sweep (measured on MI355X, tools/diag/pair_bench.py): ~110 per
+      // state slot per sweep, plus one halo exchange per block of G sweeps,
+      // ~5k cycles inside one L2, ~11k across XCDs
+      const double xchg = xcd_groupable(std::min(per, B), C) ? 5000.0 : 11000.0;
+      const double cost = nl * (110.0 * spt * G + xchg) / G;
       if (cost < best - 1e-9) {
         best = cost;
         ok = true;
@@ -788,10 +806,12 @@ int cluster_run(int mode, const ClusterPlan& plan, ClusterArgs a, int B, hipStre
   for (int b0 = 0; b0 < B; b0 += p.per_launch) {
     const int nb = std::min(p.per_launch, B - b0);
     a.b0 = b0;
-    a.xcd_group = (nb % 8 == 0) && env_int("IRLMX_XCD_GROUP", 1) != 0;
+    a.nb = nb;
+    a.xcd_group = xcd_groupable(nb, p.C) && env_int("IRLMX_XCD_GROUP", 1) != 0;
     a.salt = g_salt.fetch_add(1, std::memory_order_relaxed);
     void* args[] = {&a};
-    e = hipLaunchKernel(fn, dim3(nb * p.C), dim3(nt), args, p.lds, st);
+    const int grid = a.xcd_group ? 8 * ((nb + 7) / 8) * p.C : nb * p.C;
+    e = hipLaunchKernel(fn, dim3(grid), dim3(nt), args, p.lds, st);
     if (e != hipSuccess) return hip_fail(e, "cluster launch");
   }
   int err = 0;

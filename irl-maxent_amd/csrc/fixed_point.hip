@@ -42,6 +42,11 @@ int hip_fail(hipError_t e, const char* what);
 
 constexpr int kFusedMaxStates = 4096;
 
+static int getenv_int(const char* name, int dflt) {
+  const char* e = getenv(name);
+  return (e && *e) ? atoi(e) : dflt;
+}
+
 // Largest S run by the fused shape; IRLMX_FUSED_MAX_STATES lowers it (tests use
 // 0 to drive every size through the sweep shape).
 static int fused_max_states() {
@@ -771,6 +776,13 @@ static constexpr bool fused_pair_ok(int op, int spt, int kmax) {
 
 static bool fused_shape(const Model& m, int op, FusedShape* out) {
   if (m.S > fused_max_states() || m.A > kMaxActions) return false;
+  // Grids of width 64 / 128 run the forward and backward passes on the cluster
+  // shape even when they fit one CU: its register-resident pair layouts sweep
+  // 4-5x faster than the general-sparsity fused kernel, and a single instance
+  // then spreads over several CUs (cluster.hip).
+  if ((op == IRLMX_OP_FORWARD || op == IRLMX_OP_BACKWARD) && m.stencil && (m.W == 64 || m.W == 128) &&
+      getenv_int("IRLMX_CLUSTER", 1) != 0)
+    return false;
   const int K = op == IRLMX_OP_FORWARD ? m.Kc : m.K;
   const int kmax = pick_kmax(K);
   if (!kmax) return false;

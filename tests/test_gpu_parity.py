@@ -441,6 +441,7 @@ def test_pair_layout_bit_identical(dev, monkeypatch):
     from irlmx import DeviceMDP, ops
     keys = ("IRLMX_FUSED_MAX_STATES", "IRLMX_CLUSTER", "IRLMX_CLUSTER_R", "IRLMX_CLUSTER_G", "IRLMX_PAIR")
     shapes = {"sweep": {"IRLMX_FUSED_MAX_STATES": "0", "IRLMX_CLUSTER": "0"},
+              "no_cluster": {"IRLMX_CLUSTER": "0"},  # fused at 64 x 64, sweep at 128 x 128
               "lds": {"IRLMX_FUSED_MAX_STATES": "0", "IRLMX_PAIR": "0"},
               "rows": {"IRLMX_FUSED_MAX_STATES": "0", "IRLMX_PAIR": "1"},
               "pair": {"IRLMX_FUSED_MAX_STATES": "0"},
@@ -464,7 +465,7 @@ def test_pair_layout_bit_identical(dev, monkeypatch):
             out[name] = (pi, svf, int(k[0]))
         for k in keys:
             monkeypatch.delenv(k, raising=False)
-        for name in ("lds", "rows", "pair", "pair_small"):
+        for name in ("no_cluster", "lds", "rows", "pair", "pair_small"):
             assert torch.equal(out["sweep"][0], out[name][0]), (size, theta, name, "pi")
             assert torch.equal(out["sweep"][1], out[name][1]), (size, theta, name, "svf")
             assert out["sweep"][2] == out[name][2], (size, theta, name)
