@@ -49,6 +49,7 @@ struct ClusterPlan {
   int R, G, C, T, per_launch, spt, emax;
   size_t lds;
   int pair;             // in-tile layout: 0 per state, 1 pair rows, 2 column strips (widths 64 / 128)
+  int nt;               // threads per workgroup
 };
 
 // Tagged granules (cdna_hip_programming.md Guideline 16, form R2: the data is

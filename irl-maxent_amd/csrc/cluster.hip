@@ -675,11 +675,11 @@ static bool xcd_groupable(int nb, int C) {
   return cus >= 8 && ((nb + 7) / 8) * C <= cus / 8;
 }
 
-static size_t cluster_lds(int emax, int W, int layout) {
+static size_t cluster_lds(int emax, int W, int layout, int nt) {
   // padded ping-pong buffers (one for COLS) + the forward's block-start snapshot
   // + COLS band edge rows + summary words
   const size_t bufs = (layout == 2 ? 1 : 2) * (size_t)(emax + 2 * (W + 1)) * sizeof(double);
-  const size_t bnd = layout == 2 ? 2 * (size_t)(kPairThreads / (W / 2) + 2) * 2 * (W / 2) * 16 : 0;
+  const size_t bnd = layout == 2 ? 2 * (size_t)(nt / (W / 2) + 2) * 2 * (W / 2) * 16 : 0;
   return bufs + (size_t)emax * sizeof(double) + bnd + 64;
 }
 
@@ -694,8 +694,10 @@ bool cluster_plan(int W, int H, int B, ClusterPlan* out) {
   // layout for widths 64 / 128: IRLMX_PAIR = 2 (default) column strips, 1 pair rows, 0 per state
   const int layout = (W == 64 || W == 128) ? std::max(0, std::min(2, env_int("IRLMX_PAIR", 2))) : 0;
   const bool pair = layout > 0;
-  const int nt = pair ? kPairThreads : kCT;
-  const int spt_max = pair ? kSptMaxPair : kSptMax;
+  // column strips: IRLMX_COLS_NT = 512 (default), 768 or 1024 threads (2, 3 or 4 waves per SIMD)
+  const int cnt = env_int("IRLMX_COLS_NT", kPairThreads);
+  const int nt = layout == 2 && (cnt == 768 || cnt == 1024) ? cnt : (pair ? kPairThreads : kCT);
+  const int spt_max = pair ? kSptMaxPair * kPairThreads / nt : kSptMax;
   const int rows_cap = nt * spt_max / W;
   double best = 1e300;
   bool ok = false;
@@ -720,7 +722,7 @@ bool cluster_plan(int W, int H, int B, ClusterPlan* out) {
       if (cost < best - 1e-9) {
         best = cost;
         ok = true;
-        *out = ClusterPlan{R, G, C, G, std::min(per, B), spt, spt * nt, cluster_lds(spt * nt, W, layout), layout};
+        *out = ClusterPlan{R, G, C, G, std::min(per, B), spt, spt * nt, cluster_lds(spt * nt, W, layout, nt), layout, nt};
       }
     }
   }
@@ -755,8 +757,27 @@ static void* cluster_fn_pair(int spt) {
 
 // pair layout for widths 64 / 128 (even states per thread); compile-time LDS
 // offsets for widths 64 / 128 / 256; any other width uses WT = 0
+// column strips with 3 or 4 waves per SIMD (backward)
+template <int MODE, int WT, int NT>
+static void* cluster_fn_cols(int spt) {
+  if constexpr (MODE == kModeBwd) {
+    switch (spt) {
+      case 2: return (void*)&cluster_kernel<MODE, 2, WT, 2, NT>;
+      case 4: return (void*)&cluster_kernel<MODE, 4, WT, 2, NT>;
+      case 6: return (void*)&cluster_kernel<MODE, 6, WT, 2, NT>;
+      case 8: return NT == 768 ? (void*)&cluster_kernel<MODE, 8, WT, 2, NT == 768 ? 768 : 512> : nullptr;
+    }
+  }
+  return nullptr;
+}
+
 template <int MODE>
-static void* cluster_fn(int spt, int W, int layout) {
+static void* cluster_fn(int spt, int W, int layout, int nt) {
+  if (layout == 2 && nt != kPairThreads) {
+    if (W == 64) return nt == 768 ? cluster_fn_cols<MODE, 64, 768>(spt) : cluster_fn_cols<MODE, 64, 1024>(spt);
+    if (W == 128) return nt == 768 ? cluster_fn_cols<MODE, 128, 768>(spt) : cluster_fn_cols<MODE, 128, 1024>(spt);
+    return nullptr;
+  }
   if (layout == 1 || layout == 2) {
     if (W == 64) return layout == 1 ? cluster_fn_pair<MODE, 64, 1>(spt) : cluster_fn_pair<MODE, 64, 2>(spt);
     if (W == 128) return layout == 1 ? cluster_fn_pair<MODE, 128, 1>(spt) : cluster_fn_pair<MODE, 128, 2>(spt);
@@ -774,15 +795,17 @@ static void* cluster_fn(int spt, int W, int layout) {
 // check the exchange-timeout word (synchronises the stream).
 int cluster_run(int mode, const ClusterPlan& plan, ClusterArgs a, int B, hipStream_t st) {
   ClusterPlan p = plan;
-  if (mode == kModeFwd && p.pair == 2 && p.spt > 6) {
+  if (mode == kModeFwd && p.pair == 2 && (p.spt > 6 || p.nt != kPairThreads)) {
     // the forward's convergence bookkeeping does not fit the column-strip kernel's
     // registers at this depth: same tiles, pair-row layout
     p.pair = 1;
-    p.lds = cluster_lds(p.emax, a.W, 1);
+    p.nt = kPairThreads;
+    p.spt = p.emax / kPairThreads;
+    p.lds = cluster_lds(p.emax, a.W, 1, p.nt);
   }
   void* fn;
-  fn = mode == kModeFwd ? cluster_fn<kModeFwd>(p.spt, a.W, p.pair) : cluster_fn<kModeBwd>(p.spt, a.W, p.pair);
-  const int nt = p.pair ? kPairThreads : kCT;
+  fn = mode == kModeFwd ? cluster_fn<kModeFwd>(p.spt, a.W, p.pair, p.nt) : cluster_fn<kModeBwd>(p.spt, a.W, p.pair, p.nt);
+  const int nt = p.nt;
   if (!fn) { set_error("cluster: no kernel for spt=%d", p.spt); return IRLMX_EINVAL; }
   hipError_t e = hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)p.lds);
   if (e != hipSuccess) return hip_fail(e, "cluster hipFuncSetAttribute");
