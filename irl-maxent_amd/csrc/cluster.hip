@@ -252,93 +252,7 @@ __global__ void __launch_bounds__(NT) cluster_kernel(ClusterArgs a) {
         flags |= ((d != d) ? 1u : 0u) << (16 + i);
       }
     };
-    if constexpr (COLS) {
-      // band edge rows (old values) out, the neighbouring bands' edge rows in
-      double2* bp = bnd + (size_t)(i & 1) * (NB + 2) * 2 * HW;
-      bp[((bb + 1) * 2 + 0) * HW + cp] = make_double2(cv[0], cv[1]);
-      bp[((bb + 1) * 2 + 1) * HW + cp] = make_double2(cv[SPT - 2], cv[SPT - 1]);
-      __syncthreads();
-      const double2 above = bp[((bb + 0) * 2 + 1) * HW + cp];  // bottom row of the band above (zero band at the top)
-      const double2 below = bp[((bb + 2) * 2 + 0) * HW + cp];  // top row of the band below
-      // one row pair: old values (va, vb) of this row, up / dn = old neighbouring rows
-      auto row = [&](int jp, double2 up, double2 dn) {
-        const double va = cv[COLS ? 2 * jp : 0], vb = cv[COLS ? 2 * jp + 1 : 0];
-        const double lft = dpp_shift_f64<0x138>(vb);  // wave_shr1: left neighbour of state a
-        const double rgt = dpp_shift_f64<0x130>(va);  // wave_shl1: right neighbour of state b
-        const double* wa = w[2 * jp];
-        const double* wb = w[2 * jp + 1];
-        // the two states' chains interleaved (each in its own fixed order), so
-        // consecutive FMAs are independent
-        double acc = fma(wa[0], va, 0.0);
-        double bcc = fma(wb[0], vb, 0.0);
-        acc = fma(wa[1], vb, acc);
-        bcc = fma(wb[1], rgt, bcc);
-        acc = fma(wa[2], lft, acc);
-        bcc = fma(wb[2], va, bcc);
-        acc = fma(wa[3], dn.x, acc);
-        bcc = fma(wb[3], dn.y, bcc);
-        acc = fma(wa[4], up.x, acc);
-        bcc = fma(wb[4], up.y, bcc);
-        const double na = finish(2 * jp, acc);
-        const double nb = finish(2 * jp + 1, bcc);
-        account(2 * jp, na, va);
-        account(2 * jp + 1, nb, vb);
-        cv[COLS ? 2 * jp : 0] = na;
-        cv[COLS ? 2 * jp + 1 : 0] = nb;
-      };
-      auto old = [&](int jp) { return make_double2(cv[COLS ? 2 * jp : 0], cv[COLS ? 2 * jp + 1 : 0]); };
-      // two row pairs at once: four independent FMA chains interleaved
-      auto row2 = [&](int j1, double2 up1, double2 dn1, int j2, double2 up2, double2 dn2) {
-        const double a1 = cv[COLS ? 2 * j1 : 0], b1 = cv[COLS ? 2 * j1 + 1 : 0];
-        const double a2 = cv[COLS ? 2 * j2 : 0], b2 = cv[COLS ? 2 * j2 + 1 : 0];
-        const double l1 = dpp_shift_f64<0x138>(b1), r1 = dpp_shift_f64<0x130>(a1);
-        const double l2 = dpp_shift_f64<0x138>(b2), r2 = dpp_shift_f64<0x130>(a2);
-        const double *wa1 = w[2 * j1], *wb1 = w[2 * j1 + 1], *wa2 = w[2 * j2], *wb2 = w[2 * j2 + 1];
-        double p = fma(wa1[0], a1, 0.0), q = fma(wb1[0], b1, 0.0);
-        double u = fma(wa2[0], a2, 0.0), x = fma(wb2[0], b2, 0.0);
-        p = fma(wa1[1], b1, p);   q = fma(wb1[1], r1, q);   u = fma(wa2[1], b2, u);   x = fma(wb2[1], r2, x);
-        p = fma(wa1[2], l1, p);   q = fma(wb1[2], a1, q);   u = fma(wa2[2], l2, u);   x = fma(wb2[2], a2, x);
-        p = fma(wa1[3], dn1.x, p); q = fma(wb1[3], dn1.y, q); u = fma(wa2[3], dn2.x, u); x = fma(wb2[3], dn2.y, x);
-        p = fma(wa1[4], up1.x, p); q = fma(wb1[4], up1.y, q); u = fma(wa2[4], up2.x, u); x = fma(wb2[4], up2.y, x);
-        const double n1a = finish(2 * j1, p), n1b = finish(2 * j1 + 1, q);
-        const double n2a = finish(2 * j2, u), n2b = finish(2 * j2 + 1, x);
-        account(2 * j1, n1a, a1);
-        account(2 * j1 + 1, n1b, b1);
-        account(2 * j2, n2a, a2);
-        account(2 * j2 + 1, n2b, b2);
-        cv[COLS ? 2 * j1 : 0] = n1a;
-        cv[COLS ? 2 * j1 + 1 : 0] = n1b;
-        cv[COLS ? 2 * j2 : 0] = n2a;
-        cv[COLS ? 2 * j2 + 1 : 0] = n2b;
-      };
-      if constexpr (RW == 1) {
-        row(0, above, below);
-      } else if constexpr (RW >= 4 && RW % 2 == 0) {
-        // interior rows two at a time (no LDS operand: the edge reads above are
-        // still in flight), then the band's bottom and top rows together
-        const double2 old1 = old(1);
-        double2 prev = old(0);
-#pragma unroll
-        for (int jp = 1; jp + 1 < RW - 1; jp += 2) {
-          const double2 o1 = old(jp + 1);
-          row2(jp, prev, o1, jp + 1, old(jp), old(COLS ? min(jp + 2, RW - 1) : 0));
-          prev = o1;
-        }
-        row2(RW - 1, prev, below, 0, above, old1);
-      } else {
-        const double2 old0 = old(0), old1 = old(1);
-        double2 prev = old0;
-#pragma unroll
-        for (int jp = 1; jp < RW - 1; ++jp) {
-          const double2 cur_old = old(jp);
-          row(jp, prev, old(COLS ? min(jp + 1, RW - 1) : 0));
-          prev = cur_old;
-        }
-        row(RW - 1, prev, below);
-        row(0, above, old1);
-      }
-      return;  // no trailing barrier: the next sweep writes the other parity
-    } else if (PAIR) {
+    if constexpr (PAIR && !COLS) {
 #pragma unroll
       for (int jp = 0; jp < SPT / 2; ++jp) {
         const int l = 2 * (tid + jp * NT);
@@ -384,6 +298,71 @@ __global__ void __launch_bounds__(NT) cluster_kernel(ClusterArgs a) {
       }
     }
     __syncthreads();
+  };
+
+  // COLS sweep between two register arrays (src -> dst): no register copies for
+  // the old values the neighbouring rows still need; callers alternate the
+  // arrays, two sweeps per loop iteration.
+  double cw[COLS ? SPT : 1];
+  auto cols_sweep = [&](const double (&src)[COLS ? SPT : 1], double (&dst)[COLS ? SPT : 1], int i,
+                        unsigned& flags) {
+    if constexpr (COLS) {
+      const unsigned ob = slot_bits(own_bits);
+      auto account = [&](int j, double nv, double self) {
+        if (MODE == kModeFwd && ((ob >> j) & 1u)) {
+          const double d = fabs(nv - self);
+          flags |= ((d > eps) ? 1u : 0u) << i;
+          flags |= ((d != d) ? 1u : 0u) << (16 + i);
+        }
+      };
+      double2* bp = bnd + (size_t)(i & 1) * (NB + 2) * 2 * HW;
+      bp[((bb + 1) * 2 + 0) * HW + cp] = make_double2(src[0], src[1]);
+      bp[((bb + 1) * 2 + 1) * HW + cp] = make_double2(src[SPT - 2], src[SPT - 1]);
+      __syncthreads();
+      const double2 above = bp[((bb + 0) * 2 + 1) * HW + cp];  // bottom row of the band above (zero band at the top)
+      const double2 below = bp[((bb + 2) * 2 + 0) * HW + cp];  // top row of the band below
+      auto rowv = [&](int jp) { return make_double2(src[2 * jp], src[2 * jp + 1]); };
+      auto up_of = [&](int jp) { return jp == 0 ? above : rowv(jp > 0 ? jp - 1 : 0); };
+      auto dn_of = [&](int jp) { return jp == RW - 1 ? below : rowv(jp + 1 < RW ? jp + 1 : RW - 1); };
+      // row pairs j1 and j2 (j2 == j1: one row) at once: up to four independent
+      // FMA chains interleaved
+      auto row2 = [&](int j1, int j2) {
+        const bool two = j2 != j1;
+        const double2 up1 = up_of(j1), dn1 = dn_of(j1), up2 = up_of(j2), dn2 = dn_of(j2);
+        const double a1 = src[2 * j1], b1 = src[2 * j1 + 1];
+        const double a2 = src[2 * j2], b2 = src[2 * j2 + 1];
+        const double l1 = dpp_shift_f64<0x138>(b1), r1 = dpp_shift_f64<0x130>(a1);
+        const double *wa1 = w[2 * j1], *wb1 = w[2 * j1 + 1], *wa2 = w[2 * j2], *wb2 = w[2 * j2 + 1];
+        double p = fma(wa1[0], a1, 0.0), q = fma(wb1[0], b1, 0.0);
+        p = fma(wa1[1], b1, p);    q = fma(wb1[1], r1, q);
+        p = fma(wa1[2], l1, p);    q = fma(wb1[2], a1, q);
+        p = fma(wa1[3], dn1.x, p); q = fma(wb1[3], dn1.y, q);
+        p = fma(wa1[4], up1.x, p); q = fma(wb1[4], up1.y, q);
+        if (two) {
+          const double l2 = dpp_shift_f64<0x138>(b2), r2 = dpp_shift_f64<0x130>(a2);
+          double u = fma(wa2[0], a2, 0.0), x = fma(wb2[0], b2, 0.0);
+          u = fma(wa2[1], b2, u);    x = fma(wb2[1], r2, x);
+          u = fma(wa2[2], l2, u);    x = fma(wb2[2], a2, x);
+          u = fma(wa2[3], dn2.x, u); x = fma(wb2[3], dn2.y, x);
+          u = fma(wa2[4], up2.x, u); x = fma(wb2[4], up2.y, x);
+          dst[2 * j2] = finish(2 * j2, u);
+          dst[2 * j2 + 1] = finish(2 * j2 + 1, x);
+          account(2 * j2, dst[2 * j2], a2);
+          account(2 * j2 + 1, dst[2 * j2 + 1], b2);
+        }
+        dst[2 * j1] = finish(2 * j1, p);
+        dst[2 * j1 + 1] = finish(2 * j1 + 1, q);
+        account(2 * j1, dst[2 * j1], a1);
+        account(2 * j1 + 1, dst[2 * j1 + 1], b1);
+      };
+      // interior rows first (their operands are all in registers while the edge
+      // reads above are in flight), the band's bottom and top rows last
+#pragma unroll
+      for (int jp = 1; jp + 1 <= RW - 2; jp += 2) row2(jp, jp + 1);
+      if constexpr (RW >= 3 && (RW - 2) % 2 == 1) row2(RW - 2, RW - 2);
+      if constexpr (RW >= 2) row2(RW - 1, 0);
+      else row2(0, 0);
+    }
   };
 
   // Halo exchange in tagged granules (cluster.h): this instance's region of
@@ -445,11 +424,24 @@ __global__ void __launch_bounds__(NT) cluster_kernel(ClusterArgs a) {
     // ---- T_m sweeps on chip ----------------------------------------------
     unsigned flags = 0;
     unsigned long long mx = 0ull;
-    for (int i = 0; i < Tm; ++i) {
-      sweep(cur, oth, i, flags, 0);
-      if (!COLS) { double* t = cur; cur = oth; oth = t; }
+    if constexpr (COLS) {
+      int i = 0;
+      for (; i + 1 < Tm; i += 2) {
+        cols_sweep(cv, cw, i, flags);
+        cols_sweep(cw, cv, i + 1, flags);
+      }
+      if (i < Tm) {
+        cols_sweep(cv, cw, i, flags);
+#pragma unroll
+        for (int j = 0; j < (COLS ? SPT : 1); ++j) cv[j] = cw[j];
+      }
+      __syncthreads();  // the last sweep's boundary reads are done
+    } else {
+      for (int i = 0; i < Tm; ++i) {
+        sweep(cur, oth, i, flags, 0);
+        double* t = cur; cur = oth; oth = t;
+      }
     }
-    if (COLS) __syncthreads();  // the last sweep's boundary reads are done
     if (MODE == kModeBwd && a.rescale) {  // owned maximum of the block's last sweep
       const unsigned ob = slot_bits(own_bits);
 #pragma unroll
@@ -540,9 +532,22 @@ __global__ void __launch_bounds__(NT) cluster_kernel(ClusterArgs a) {
         __syncthreads();
         reload(cur);
         unsigned scratch = 0;
-        for (int i = 0; i < conv; ++i) {
-          sweep(cur, oth, i, scratch, 0);
-          if (!COLS) { double* t = cur; cur = oth; oth = t; }
+        if constexpr (COLS) {
+          int i = 0;
+          for (; i + 1 < conv; i += 2) {
+            cols_sweep(cv, cw, i, scratch);
+            cols_sweep(cw, cv, i + 1, scratch);
+          }
+          if (i < conv) {
+            cols_sweep(cv, cw, i, scratch);
+#pragma unroll
+            for (int j = 0; j < (COLS ? SPT : 1); ++j) cv[j] = cw[j];
+          }
+        } else {
+          for (int i = 0; i < conv; ++i) {
+            sweep(cur, oth, i, scratch, 0);
+            double* t = cur; cur = oth; oth = t;
+          }
         }
         if (COLS) {
           const unsigned ob = slot_bits(own_bits);
