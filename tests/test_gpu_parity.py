@@ -469,3 +469,43 @@ def test_pair_layout_bit_identical(dev, monkeypatch):
             assert torch.equal(out["sweep"][0], out[name][0]), (size, theta, name, "pi")
             assert torch.equal(out["sweep"][1], out[name][1]), (size, theta, name, "svf")
             assert out["sweep"][2] == out[name][2], (size, theta, name)
+
+
+def test_cluster_multi_launch_and_edge_cases(dev, monkeypatch):
+    """Cluster shape with more instances than one launch holds (forced 2-row
+    tiles: C = 32, 8 instances per launch, B = 11 -> launches of 8 and of 3, the
+    second on a padded XCD-grouped grid), instances that stop at different
+    sweeps, one with a NaN policy (stops after one sweep, NONFINITE) and a
+    max_iter cap -- bit-identical to the per-sweep shape."""
+    from irlmx import DeviceMDP, ops
+    size, B = 64, 11
+    n = size * size
+    slips = np.linspace(0.05, 0.4, B)
+    mdp = DeviceMDP.icy_gridworld(size, slips, device=dev)
+    rng = np.random.default_rng(21)
+    r = rng.uniform(0.0, 1.0, (B, n))
+    tm = ops.terminal_mask([n - 1], n, batch=B, device=dev)
+    p0 = np.zeros((B, n))
+    p0[np.arange(B), rng.integers(0, n - 1, B)] = 1.0
+    keys = ("IRLMX_FUSED_MAX_STATES", "IRLMX_CLUSTER", "IRLMX_CLUSTER_R", "IRLMX_CLUSTER_G")
+    out = {}
+    for name, env in (("sweep", {"IRLMX_FUSED_MAX_STATES": "0", "IRLMX_CLUSTER": "0"}),
+                      ("cluster", {"IRLMX_CLUSTER_R": "2", "IRLMX_CLUSTER_G": "5"})):
+        for k in keys:
+            monkeypatch.delenv(k, raising=False)
+        for k, v in env.items():
+            monkeypatch.setenv(k, v)
+        pi = ops.backward_maxent(mdp, r, tm)
+        pi[3, 17, 2] = float("nan")   # instance 3: non-finite policy
+        svf, k, st = ops.forward_svf(mdp, p0, tm, pi, max_iter=3000)
+        out[name] = (pi, svf, k, st)
+    for k in keys:
+        monkeypatch.delenv(k, raising=False)
+    a, b = out["sweep"], out["cluster"]
+    assert torch.equal(a[0][~torch.isnan(a[0])], b[0][~torch.isnan(b[0])])
+    assert torch.equal(a[2], b[2]) and torch.equal(a[3], b[3]), (a[2].tolist(), b[2].tolist())
+    fin = torch.isfinite(a[1])
+    assert torch.equal(fin, torch.isfinite(b[1])) and torch.equal(a[1][fin], b[1][fin])
+    assert int(b[2][3]) == 1 and int(b[3][3]) == 1                 # NaN policy: one sweep, NONFINITE
+    assert torch.isnan(b[1][3]).all()
+    assert len(set(b[2].tolist())) > 2                                # instances stop at different sweeps
