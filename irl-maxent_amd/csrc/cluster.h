@@ -12,7 +12,9 @@ constexpr int kCT = 1024;          // threads per workgroup, per-state layout
 constexpr int kSptMax = 6;         // states per thread, per-state layout (no VGPR spills at 128 VGPRs)
 constexpr int kPairThreads = 512;  // threads per workgroup, pair layouts (256 VGPRs)
 constexpr int kSptMaxPair = 12;    // states per thread, pair layouts -> extended tile <= 6144 states
+constexpr int kSptMaxQuadFwd = 8;  // forward with column quads (register budget)
 constexpr int kTMax = 16;          // max sweeps per block (= max ghost rows)
+constexpr size_t kMaxLdsBytes = 160 * 1024;  // LDS per CU (one workgroup per CU)
 constexpr int kModeFwd = 0;
 constexpr int kModeBwd = 1;
 
@@ -48,7 +50,7 @@ struct ClusterArgs {
 struct ClusterPlan {
   int R, G, C, T, per_launch, spt, emax;
   size_t lds;
-  int pair;             // in-tile layout: 0 per state, 1 pair rows, 2 column strips (widths 64 / 128)
+  int pair;             // in-tile layout: 0 per state, 1 pair rows, 2 column pairs, 3 column quads
   int nt;               // threads per workgroup
 };
 
@@ -140,7 +142,7 @@ __device__ inline unsigned long long wave_or_u64(unsigned long long v) {
   return v;
 }
 
-bool cluster_plan(int W, int H, int B, ClusterPlan* out);
+bool cluster_plan(int W, int H, int B, int mode, ClusterPlan* out);
 int cluster_run(int mode, const ClusterPlan& p, ClusterArgs a, int B, hipStream_t st);
 __global__ void bwd_growth_kernel(const double* __restrict__ bw, int S, unsigned long long* __restrict__ growth);
 

@@ -89,13 +89,20 @@ __device__ inline double dpp_shift_f64(double x) {
 // except at the band's top and bottom row, which go through a small
 // double-buffered LDS boundary array -- per sweep one 16-byte write and one
 // read at each band edge instead of three 16-byte accesses per pair.
+//
+// LAY == 3 is the same with four columns per lane (CPL = 4): half the DPP
+// moves per state, and at width 256 one band row is one wave.
 template <int MODE, int SPT, int WT, int LAY, int NT>
 __global__ void __launch_bounds__(NT) cluster_kernel(ClusterArgs a) {
-  constexpr bool PAIR = LAY >= 1, COLS = LAY == 2;
-  static_assert(!PAIR || (SPT % 2 == 0 && (WT == 64 || WT == 128)), "pair layouts: even SPT, width 64/128");
-  constexpr int RW = SPT / 2;                            // COLS: rows per band
-  constexpr int HW = WT / 2;                             // COLS: lanes per band (column pairs per row)
-  constexpr int NB = COLS ? NT / (WT ? HW : 1) : 1;      // COLS: bands
+  constexpr bool PAIR = LAY >= 1, COLS = LAY >= 2;
+  constexpr int CPL = LAY == 3 ? 4 : 2;                  // COLS: columns per lane
+  static_assert(LAY != 1 || (SPT % 2 == 0 && (WT == 64 || WT == 128)), "pair rows: even SPT, width 64/128");
+  static_assert(LAY != 2 || (SPT % 2 == 0 && (WT == 64 || WT == 128)), "column pairs: even SPT, width 64/128");
+  static_assert(LAY != 3 || (SPT % 4 == 0 && (WT == 128 || WT == 256)), "column quads: SPT % 4, width 128/256");
+  constexpr int RW = COLS ? SPT / CPL : 1;               // COLS: rows per band
+  constexpr int HW = COLS ? WT / CPL : 1;                // COLS: lanes per band
+  constexpr int NB = COLS ? NT / HW : 1;                 // COLS: bands
+  constexpr int QW = CPL / 2;                            // COLS: double2 per lane per row
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   const int W = WT ? WT : a.W;
   const int H = a.H, S = a.S;
@@ -124,18 +131,19 @@ __global__ void __launch_bounds__(NT) cluster_kernel(ClusterArgs a) {
   const int base = e0 * W;
   const int pad = PAIR ? W : W + 1;  // pair layout keeps every pair 16-byte aligned
   const int blen = a.emax + 2 * pad;
-  const int cp = COLS ? tid % HW : 0, bb = COLS ? tid / HW : 0;  // COLS: column pair, band
+  const int cp = COLS ? tid % HW : 0, bb = COLS ? tid / HW : 0;  // COLS: column group, band
   // state index of register slot j
   auto slot_state = [&](int j) {
-    if (COLS) return (bb * RW + (j >> 1)) * W + 2 * cp + (j & 1);
+    if (COLS) return (bb * RW + j / CPL) * W + CPL * cp + j % CPL;
     return PAIR ? 2 * (tid + (j >> 1) * NT) + (j & 1) : tid + j * NT;
   };
   double* bufA = (double*)smem;
-  double* bufB = bufA + (COLS ? 0 : blen);  // COLS keeps one buffer (ghost staging, final sweep)
+  // COLS keeps a single tile buffer (ghost staging, the backward's final sweep)
+  double* bufB = bufA + (COLS ? 0 : blen);
   double* snap = bufB + blen;                                            // forward: block-start state
-  // COLS: band edge rows [2 parities][NB + 2 (zero band at both ends)][2: top, bottom][HW] pairs
+  // COLS: band edge rows [2 parities][NB + 2 (zero band at both ends)][2: top, bottom][HW][QW] double2
   double2* bnd = (double2*)(snap + (MODE == kModeFwd ? a.emax : 0));
-  constexpr int kBndLen = COLS ? 2 * (NB + 2) * 2 * HW : 0;
+  constexpr int kBndLen = COLS ? 2 * (NB + 2) * 2 * HW * QW : 0;
   unsigned long long* red = (unsigned long long*)(bnd + kBndLen);  // [3]
   int* lflag = (int*)(red + 3);                                          // [4]
 
@@ -209,10 +217,11 @@ __global__ void __launch_bounds__(NT) cluster_kernel(ClusterArgs a) {
   }
 
   // Opaque per use, so the compiler does not hoist per-slot SGPR masks out of
-  // the loops (SGPR pressure).  With the pair layouts at width 128 a wave
-  // covers exactly one row per slot, so the predicates are wave-uniform: kept
-  // in an SGPR they turn into scalar branches instead of per-lane selects.
-  constexpr bool kUniformSlots = PAIR && WT == 128;
+  // the loops (SGPR pressure).  When a wave covers exactly one row per slot
+  // (pair rows at width 128; column strips with 64 lanes per band row) the
+  // predicates are wave-uniform: kept in an SGPR they turn into scalar
+  // branches instead of per-lane selects.
+  constexpr bool kUniformSlots = LAY == 1 ? WT == 128 : (COLS && HW == 64);
   auto slot_bits = [&](unsigned b) {
     if constexpr (kUniformSlots) {
       b = (unsigned)__builtin_amdgcn_readfirstlane((int)b);
@@ -304,6 +313,9 @@ __global__ void __launch_bounds__(NT) cluster_kernel(ClusterArgs a) {
   // the old values the neighbouring rows still need; callers alternate the
   // arrays, two sweeps per loop iteration.
   double cw[COLS ? SPT : 1];
+  // band edge row e (0: top, 1: bottom) of band slot `band` (0 and NB + 1 are
+  // the zero bands) in parity buffer `par`
+  auto bnd_at = [&](int par, int band, int e) { return bnd + ((((size_t)par * (NB + 2) + band) * 2 + e) * HW + cp) * QW; };
   auto cols_sweep = [&](const double (&src)[COLS ? SPT : 1], double (&dst)[COLS ? SPT : 1], int i,
                         unsigned& flags) {
     if constexpr (COLS) {
@@ -315,53 +327,70 @@ __global__ void __launch_bounds__(NT) cluster_kernel(ClusterArgs a) {
           flags |= ((d != d) ? 1u : 0u) << (16 + i);
         }
       };
-      double2* bp = bnd + (size_t)(i & 1) * (NB + 2) * 2 * HW;
-      bp[((bb + 1) * 2 + 0) * HW + cp] = make_double2(src[0], src[1]);
-      bp[((bb + 1) * 2 + 1) * HW + cp] = make_double2(src[SPT - 2], src[SPT - 1]);
-      __syncthreads();
-      const double2 above = bp[((bb + 0) * 2 + 1) * HW + cp];  // bottom row of the band above (zero band at the top)
-      const double2 below = bp[((bb + 2) * 2 + 0) * HW + cp];  // top row of the band below
-      auto rowv = [&](int jp) { return make_double2(src[2 * jp], src[2 * jp + 1]); };
-      auto up_of = [&](int jp) { return jp == 0 ? above : rowv(jp > 0 ? jp - 1 : 0); };
-      auto dn_of = [&](int jp) { return jp == RW - 1 ? below : rowv(jp + 1 < RW ? jp + 1 : RW - 1); };
-      // row pairs j1 and j2 (j2 == j1: one row) at once: up to four independent
-      // FMA chains interleaved
-      auto row2 = [&](int j1, int j2) {
-        const bool two = j2 != j1;
-        const double2 up1 = up_of(j1), dn1 = dn_of(j1), up2 = up_of(j2), dn2 = dn_of(j2);
-        const double a1 = src[2 * j1], b1 = src[2 * j1 + 1];
-        const double a2 = src[2 * j2], b2 = src[2 * j2 + 1];
-        const double l1 = dpp_shift_f64<0x138>(b1), r1 = dpp_shift_f64<0x130>(a1);
-        const double *wa1 = w[2 * j1], *wb1 = w[2 * j1 + 1], *wa2 = w[2 * j2], *wb2 = w[2 * j2 + 1];
-        double p = fma(wa1[0], a1, 0.0), q = fma(wb1[0], b1, 0.0);
-        p = fma(wa1[1], b1, p);    q = fma(wb1[1], r1, q);
-        p = fma(wa1[2], l1, p);    q = fma(wb1[2], a1, q);
-        p = fma(wa1[3], dn1.x, p); q = fma(wb1[3], dn1.y, q);
-        p = fma(wa1[4], up1.x, p); q = fma(wb1[4], up1.y, q);
-        if (two) {
-          const double l2 = dpp_shift_f64<0x138>(b2), r2 = dpp_shift_f64<0x130>(a2);
-          double u = fma(wa2[0], a2, 0.0), x = fma(wb2[0], b2, 0.0);
-          u = fma(wa2[1], b2, u);    x = fma(wb2[1], r2, x);
-          u = fma(wa2[2], l2, u);    x = fma(wb2[2], a2, x);
-          u = fma(wa2[3], dn2.x, u); x = fma(wb2[3], dn2.y, x);
-          u = fma(wa2[4], up2.x, u); x = fma(wb2[4], up2.y, x);
-          dst[2 * j2] = finish(2 * j2, u);
-          dst[2 * j2 + 1] = finish(2 * j2 + 1, x);
-          account(2 * j2, dst[2 * j2], a2);
-          account(2 * j2 + 1, dst[2 * j2 + 1], b2);
+      {  // band edge rows (old values) out
+        double2* t = bnd_at(i & 1, bb + 1, 0);
+        double2* u = bnd_at(i & 1, bb + 1, 1);
+#pragma unroll
+        for (int q = 0; q < QW; ++q) {
+          t[q] = make_double2(src[2 * q], src[2 * q + 1]);
+          u[q] = make_double2(src[SPT - CPL + 2 * q], src[SPT - CPL + 2 * q + 1]);
         }
-        dst[2 * j1] = finish(2 * j1, p);
-        dst[2 * j1 + 1] = finish(2 * j1 + 1, q);
-        account(2 * j1, dst[2 * j1], a1);
-        account(2 * j1 + 1, dst[2 * j1 + 1], b1);
+      }
+      __syncthreads();
+      double above[CPL], below[CPL];  // bottom row of the band above, top row of the band below
+      {
+        const double2* t = bnd_at(i & 1, bb, 1);
+        const double2* u = bnd_at(i & 1, bb + 2, 0);
+#pragma unroll
+        for (int q = 0; q < QW; ++q) {
+          const double2 x = t[q], y = u[q];
+          above[2 * q] = x.x; above[2 * q + 1] = x.y;
+          below[2 * q] = y.x; below[2 * q + 1] = y.y;
+        }
+      }
+      // rows j1 and j2 (j2 == j1: one row) at once: up to 2 * CPL independent FMA chains
+      auto rows = [&](int j1, int j2) {
+        const bool two = j2 != j1;
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+          if (h == 1 && !two) break;
+          const int jr = h == 0 ? j1 : j2;
+          const double* v = src + jr * CPL;
+          const double* up = jr == 0 ? above : src + (jr > 0 ? jr - 1 : 0) * CPL;
+          const double* dn = jr == RW - 1 ? below : src + (jr + 1 < RW ? jr + 1 : RW - 1) * CPL;
+          const double lft = dpp_shift_f64<0x138>(v[CPL - 1]);  // wave_shr1: left of column 0
+          const double rgt = dpp_shift_f64<0x130>(v[0]);        // wave_shl1: right of column CPL - 1
+          double acc[CPL];
+#pragma unroll
+          for (int c = 0; c < CPL; ++c) acc[c] = fma(w[jr * CPL + c][0], v[c], 0.0);
+#pragma unroll
+          for (int c = 0; c < CPL; ++c) acc[c] = fma(w[jr * CPL + c][1], c + 1 < CPL ? v[c + 1 < CPL ? c + 1 : 0] : rgt, acc[c]);
+#pragma unroll
+          for (int c = 0; c < CPL; ++c) acc[c] = fma(w[jr * CPL + c][2], c > 0 ? v[c > 0 ? c - 1 : 0] : lft, acc[c]);
+#pragma unroll
+          for (int c = 0; c < CPL; ++c) acc[c] = fma(w[jr * CPL + c][3], dn[c], acc[c]);
+#pragma unroll
+          for (int c = 0; c < CPL; ++c) acc[c] = fma(w[jr * CPL + c][4], up[c], acc[c]);
+#pragma unroll
+          for (int c = 0; c < CPL; ++c) {
+            dst[jr * CPL + c] = finish(jr * CPL + c, acc[c]);
+            account(jr * CPL + c, dst[jr * CPL + c], v[c]);
+          }
+        }
       };
       // interior rows first (their operands are all in registers while the edge
-      // reads above are in flight), the band's bottom and top rows last
+      // reads above are in flight), the band's bottom and top rows last; with
+      // two columns per lane, two rows at a time
+      constexpr int step = CPL == 2 ? 2 : 1;
 #pragma unroll
-      for (int jp = 1; jp + 1 <= RW - 2; jp += 2) row2(jp, jp + 1);
-      if constexpr (RW >= 3 && (RW - 2) % 2 == 1) row2(RW - 2, RW - 2);
-      if constexpr (RW >= 2) row2(RW - 1, 0);
-      else row2(0, 0);
+      for (int jp = 1; jp + step - 1 <= RW - 2; jp += step) rows(jp, jp + step - 1);
+      if constexpr (step == 2 && RW >= 3 && (RW - 2) % 2 == 1) rows(RW - 2, RW - 2);
+      if constexpr (RW >= 2) {
+        if constexpr (CPL == 2) rows(RW - 1, 0);
+        else { rows(RW - 1, RW - 1); rows(0, 0); }
+      } else {
+        rows(0, 0);
+      }
     }
   };
 
@@ -455,17 +484,29 @@ __global__ void __launch_bounds__(NT) cluster_kernel(ClusterArgs a) {
     // ---- publish the halo rows, tagged with the block ------------------------
     const unsigned tag = salt | (((unsigned)m + 1u) & 0xFFFFFu);
     const unsigned gpar = (unsigned)(m & 1) * (unsigned)S;
-    if constexpr (PAIR) {
+    auto store_rows = [&]() {  // from the LDS tile, spread evenly over all threads
+      for (int l = own0 + tid; l < pubA1; l += NT)
+        gran_store(rg, (gpar + (unsigned)(base + l)) * 16u, dbits(cur[pad + l]), tag, plain);
+      for (int l = pubB0 + tid; l < own1; l += NT)
+        gran_store(rg, (gpar + (unsigned)(base + l)) * 16u, dbits(cur[pad + l]), tag, plain);
+    };
+    if constexpr (COLS) {
+      // a band's rows sit in one wave: stage them in the LDS tile first, so that
+      // the stores spread over all waves after the barrier below
+      const unsigned pb = slot_bits(pub_bits);
+#pragma unroll
+      for (int jp = 0; jp < SPT / 2; ++jp)
+        if ((pb >> (2 * jp)) & 1u)
+          *reinterpret_cast<double2*>(cur + pad + slot_state(2 * jp)) =
+              make_double2(cv[PAIR ? 2 * jp : 0], cv[PAIR ? 2 * jp + 1 : 0]);
+    } else if constexpr (PAIR) {
       const unsigned pb = slot_bits(pub_bits);
 #pragma unroll
       for (int j = 0; j < SPT; ++j)  // per register slot: all stores of a thread in flight together
         if ((pb >> j) & 1u)
           gran_store(rg, (gpar + (unsigned)(base + slot_state(j))) * 16u, dbits(cv[PAIR ? j : 0]), tag, plain);
     } else {
-      for (int l = own0 + tid; l < pubA1; l += NT)
-        gran_store(rg, (gpar + (unsigned)(base + l)) * 16u, dbits(cur[pad + l]), tag, plain);
-      for (int l = pubB0 + tid; l < own1; l += NT)
-        gran_store(rg, (gpar + (unsigned)(base + l)) * 16u, dbits(cur[pad + l]), tag, plain);
+      store_rows();
     }
     if (stamps) { const unsigned long long t = stamp_now(); st_acc[5] += t - ts; }
     // ---- per-tile summary of the block (32 bits), while the halo is in flight --
@@ -481,8 +522,9 @@ __global__ void __launch_bounds__(NT) cluster_kernel(ClusterArgs a) {
       if ((tid & (kWave - 1)) == 0 && wc) atomicMax(&red32[m & 1], wc);
     }
     if (stamps) { const unsigned long long t = stamp_now(); st_acc[6] += t - ts; }
-    __syncthreads();  // the tile summary in red32[m & 1] is complete
+    __syncthreads();  // the tile summary in red32[m & 1] (and COLS: the staged rows) complete
     if (tid == 0) gran_store(rs, ((unsigned)(m & 1) * (unsigned)a.H + (unsigned)tile) * 16u, red32[m & 1], tag, plain);
+    if constexpr (COLS) store_rows();
     stamp(1);
     // ---- gather this tile's ghost rows and (threads < C) every tile's summary,
     // ---- all polls of a thread in flight together: one round trip --------------
@@ -680,29 +722,42 @@ static bool xcd_groupable(int nb, int C) {
   return cus >= 8 && ((nb + 7) / 8) * C <= cus / 8;
 }
 
-static size_t cluster_lds(int emax, int W, int layout, int nt) {
-  // padded ping-pong buffers (one for COLS) + the forward's block-start snapshot
-  // + COLS band edge rows + summary words
-  const size_t bufs = (layout == 2 ? 1 : 2) * (size_t)(emax + 2 * (W + 1)) * sizeof(double);
-  const size_t bnd = layout == 2 ? 2 * (size_t)(nt / (W / 2) + 2) * 2 * (W / 2) * 16 : 0;
-  return bufs + (size_t)emax * sizeof(double) + bnd + 64;
+static size_t cluster_lds(int emax, int W, int layout, int nt, int mode) {
+  const size_t buf = (size_t)(emax + 2 * (W + 1)) * sizeof(double);  // one padded tile buffer
+  const size_t snap = mode == kModeFwd ? (size_t)emax * sizeof(double) : 0;  // forward block-start state
+  if (layout >= 2) {
+    // column strips: one tile buffer (ghost staging, final sweep) + snapshot +
+    // band edge rows [2][NB + 2][2][W / CPL lanes] of CPL doubles + summary words
+    const int cpl = layout == 3 ? 4 : 2;
+    const size_t bnd = 2 * (size_t)(nt / (W / cpl) + 2) * 2 * W * sizeof(double);
+    return buf + snap + bnd + 64;
+  }
+  // ping-pong buffers + snapshot + summary words
+  return 2 * buf + snap + 64;
 }
 
 // Tile plan for a width x height stencil grid and B instances: the fewest
 // sequential launches first, then the most sweeps per exchange (G), then the
 // smallest extended tile.  IRLMX_CLUSTER_R / _G force a plan (tests).
-bool cluster_plan(int W, int H, int B, ClusterPlan* out) {
+bool cluster_plan(int W, int H, int B, int mode, ClusterPlan* out) {
   if (env_int("IRLMX_CLUSTER", 1) == 0) return false;
   const int cus = device_cus();
   if (cus <= 0) return false;
   const int fR = env_int("IRLMX_CLUSTER_R", 0), fG = env_int("IRLMX_CLUSTER_G", 0);
   // layout for widths 64 / 128: IRLMX_PAIR = 2 (default) column strips, 1 pair rows, 0 per state
-  const int layout = (W == 64 || W == 128) ? std::max(0, std::min(2, env_int("IRLMX_PAIR", 2))) : 0;
+  // in-tile layout (IRLMX_PAIR forces one): widths 64 / 128 column pairs (2;
+  // 1 = pair rows, 3 = column quads at 128), width 256 backward column quads
+  // (3), other widths per state (0)
+  int layout = 0;
+  const int env_layout = env_int("IRLMX_PAIR", -1);
+  if (W == 64 || W == 128) layout = env_layout >= 0 ? std::min(env_layout, W == 128 ? 3 : 2) : 2;
+  // (the forward's column quads fit only 8 states per lane: too few rows per
+  // tile at width 256, so its forward stays per state)
+  if (W == 256) layout = env_layout >= 0 ? (env_layout == 3 ? 3 : 0) : (mode == kModeBwd ? 3 : 0);
   const bool pair = layout > 0;
-  // column strips: IRLMX_COLS_NT = 512 (default), 768 or 1024 threads (2, 3 or 4 waves per SIMD)
-  const int cnt = env_int("IRLMX_COLS_NT", kPairThreads);
-  const int nt = layout == 2 && (cnt == 768 || cnt == 1024) ? cnt : (pair ? kPairThreads : kCT);
-  const int spt_max = pair ? kSptMaxPair * kPairThreads / nt : kSptMax;
+  const int nt = pair ? kPairThreads : kCT;
+  // register budget per lane: the forward's convergence bookkeeping needs more
+  const int spt_max = !pair ? kSptMax : (mode == kModeFwd && layout == 3 ? kSptMaxQuadFwd : kSptMaxPair);
   const int rows_cap = nt * spt_max / W;
   double best = 1e300;
   bool ok = false;
@@ -714,8 +769,9 @@ bool cluster_plan(int W, int H, int B, ClusterPlan* out) {
       const int ext = std::min(H, R + 2 * G);
       const int E = ext * W;
       int spt = (E + nt - 1) / nt;
-      if (pair && (spt & 1)) ++spt;
+      if (pair) spt = (spt + (layout == 3 ? 3 : 1)) / (layout == 3 ? 4 : 2) * (layout == 3 ? 4 : 2);
       if (spt > spt_max) continue;
+      if (cluster_lds(spt * nt, W, layout, nt, mode) > kMaxLdsBytes) continue;
       const int per = cus / C;
       if (per < 1) continue;
       const int nl = (B + per - 1) / per;
@@ -727,7 +783,7 @@ bool cluster_plan(int W, int H, int B, ClusterPlan* out) {
       if (cost < best - 1e-9) {
         best = cost;
         ok = true;
-        *out = ClusterPlan{R, G, C, G, std::min(per, B), spt, spt * nt, cluster_lds(spt * nt, W, layout, nt), layout, nt};
+        *out = ClusterPlan{R, G, C, G, std::min(per, B), spt, spt * nt, cluster_lds(spt * nt, W, layout, nt, mode), layout, nt};
       }
     }
   }
@@ -762,25 +818,21 @@ static void* cluster_fn_pair(int spt) {
 
 // pair layout for widths 64 / 128 (even states per thread); compile-time LDS
 // offsets for widths 64 / 128 / 256; any other width uses WT = 0
-// column strips with 3 or 4 waves per SIMD (backward)
-template <int MODE, int WT, int NT>
-static void* cluster_fn_cols(int spt) {
-  if constexpr (MODE == kModeBwd) {
-    switch (spt) {
-      case 2: return (void*)&cluster_kernel<MODE, 2, WT, 2, NT>;
-      case 4: return (void*)&cluster_kernel<MODE, 4, WT, 2, NT>;
-      case 6: return (void*)&cluster_kernel<MODE, 6, WT, 2, NT>;
-      case 8: return NT == 768 ? (void*)&cluster_kernel<MODE, 8, WT, 2, NT == 768 ? 768 : 512> : nullptr;
-    }
+template <int MODE, int WT>
+static void* cluster_fn_quad(int spt) {
+  switch (spt) {
+    case 4: return (void*)&cluster_kernel<MODE, 4, WT, 3, kPairThreads>;
+    case 8: return (void*)&cluster_kernel<MODE, 8, WT, 3, kPairThreads>;
+    case 12: return MODE == kModeBwd ? (void*)&cluster_kernel<MODE, 12, WT, 3, kPairThreads> : nullptr;
   }
   return nullptr;
 }
 
 template <int MODE>
-static void* cluster_fn(int spt, int W, int layout, int nt) {
-  if (layout == 2 && nt != kPairThreads) {
-    if (W == 64) return nt == 768 ? cluster_fn_cols<MODE, 64, 768>(spt) : cluster_fn_cols<MODE, 64, 1024>(spt);
-    if (W == 128) return nt == 768 ? cluster_fn_cols<MODE, 128, 768>(spt) : cluster_fn_cols<MODE, 128, 1024>(spt);
+static void* cluster_fn(int spt, int W, int layout, int) {
+  if (layout == 3) {
+    if (W == 128) return cluster_fn_quad<MODE, 128>(spt);
+    if (W == 256) return cluster_fn_quad<MODE, 256>(spt);
     return nullptr;
   }
   if (layout == 1 || layout == 2) {
@@ -800,13 +852,13 @@ static void* cluster_fn(int spt, int W, int layout, int nt) {
 // check the exchange-timeout word (synchronises the stream).
 int cluster_run(int mode, const ClusterPlan& plan, ClusterArgs a, int B, hipStream_t st) {
   ClusterPlan p = plan;
-  if (mode == kModeFwd && p.pair == 2 && (p.spt > 6 || p.nt != kPairThreads)) {
+  if (mode == kModeFwd && p.pair == 2 && p.spt > 6) {
     // the forward's convergence bookkeeping does not fit the column-strip kernel's
     // registers at this depth: same tiles, pair-row layout
     p.pair = 1;
     p.nt = kPairThreads;
     p.spt = p.emax / kPairThreads;
-    p.lds = cluster_lds(p.emax, a.W, 1, p.nt);
+    p.lds = cluster_lds(p.emax, a.W, 1, p.nt, mode);
   }
   void* fn;
   fn = mode == kModeFwd ? cluster_fn<kModeFwd>(p.spt, a.W, p.pair, p.nt) : cluster_fn<kModeBwd>(p.spt, a.W, p.pair, p.nt);
@@ -853,7 +905,7 @@ int cluster_run(int mode, const ClusterPlan& plan, ClusterArgs a, int B, hipStre
     for (int g = 0; g < nwg; ++g)
       for (int k = 0; k < 8; ++k) acc[k] += (double)h[(size_t)g * 8 + k] / nwg;
     fprintf(stderr, "[irlmx stamps] %s%s mode=%d R=%d G=%d C=%d spt=%d blocks=%.0f  cycles/block: sweeps %.0f  publish %.0f  "
-                    "wait %.0f  refresh %.0f  same-xcd %.2f  (publish: stores %.0f, summary %.0f)\n", "lds", p.pair == 2 ? "-cols" : (p.pair == 1 ? "-pair" : ""), mode, p.R, p.G, p.C, p.spt,
+                    "wait %.0f  refresh %.0f  same-xcd %.2f  (publish: stores %.0f, summary %.0f)\n", "lds", p.pair == 3 ? "-quads" : (p.pair == 2 ? "-cols" : (p.pair == 1 ? "-pair" : "")), mode, p.R, p.G, p.C, p.spt,
             acc[4], acc[0] / acc[4], acc[1] / acc[4], acc[2] / acc[4], acc[3] / acc[4], acc[5], acc[6] / acc[4],
             (acc[7] - acc[6]) / acc[4]);
     free(h);

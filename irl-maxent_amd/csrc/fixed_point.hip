@@ -919,7 +919,7 @@ extern "C" int irlmx_forward_svf(const irlmx_mdp* mdp, const double* p_initial, 
     return 0;
   }
   ClusterPlan cp;
-  if (m.stencil && cluster_plan(m.W, m.H, m.B, &cp)) {
+  if (m.stencil && cluster_plan(m.W, m.H, m.B, kModeFwd, &cp)) {
     ClusterArgs ca{};
     ca.W = m.W; ca.H = m.H; ca.S = m.S; ca.A = m.A;
     ca.wgt = ws.wgt; ca.vin = p_initial; ca.bad = ws.bad;
@@ -956,7 +956,7 @@ extern "C" int irlmx_backward_maxent(const irlmx_mdp* mdp, const double* reward,
     return 0;
   }
   ClusterPlan cp;
-  if (m.stencil && m.A <= kMaxActions && cluster_plan(m.W, m.H, m.B, &cp)) {
+  if (m.stencil && m.A <= kMaxActions && cluster_plan(m.W, m.H, m.B, kModeBwd, &cp)) {
     hipLaunchKernelGGL(bwd_growth_kernel, dim3(m.B), dim3(1024), 0, st, ws.wgt, m.S, ws.growth);
     ClusterArgs ca{};
     ca.W = m.W; ca.H = m.H; ca.S = m.S; ca.A = m.A;

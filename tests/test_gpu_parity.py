@@ -444,6 +444,7 @@ def test_pair_layout_bit_identical(dev, monkeypatch):
               "no_cluster": {"IRLMX_CLUSTER": "0"},  # fused at 64 x 64, sweep at 128 x 128
               "lds": {"IRLMX_FUSED_MAX_STATES": "0", "IRLMX_PAIR": "0"},
               "rows": {"IRLMX_FUSED_MAX_STATES": "0", "IRLMX_PAIR": "1"},
+              "quads": {"IRLMX_FUSED_MAX_STATES": "0", "IRLMX_PAIR": "3"},  # width 128 only (else column pairs)
               "pair": {"IRLMX_FUSED_MAX_STATES": "0"},
               "pair_small": {"IRLMX_FUSED_MAX_STATES": "0", "IRLMX_CLUSTER_R": "7", "IRLMX_CLUSTER_G": "3"}}
     rng = np.random.default_rng(5)
@@ -465,7 +466,7 @@ def test_pair_layout_bit_identical(dev, monkeypatch):
             out[name] = (pi, svf, int(k[0]))
         for k in keys:
             monkeypatch.delenv(k, raising=False)
-        for name in ("no_cluster", "lds", "rows", "pair", "pair_small"):
+        for name in ("no_cluster", "lds", "rows", "quads", "pair", "pair_small"):
             assert torch.equal(out["sweep"][0], out[name][0]), (size, theta, name, "pi")
             assert torch.equal(out["sweep"][1], out[name][1]), (size, theta, name, "svf")
             assert out["sweep"][2] == out[name][2], (size, theta, name)
@@ -509,3 +510,35 @@ def test_cluster_multi_launch_and_edge_cases(dev, monkeypatch):
     assert int(b[2][3]) == 1 and int(b[3][3]) == 1                 # NaN policy: one sweep, NONFINITE
     assert torch.isnan(b[1][3]).all()
     assert len(set(b[2].tolist())) > 2                                # instances stop at different sweeps
+
+
+def test_width256_quads_bit_identical(dev, monkeypatch):
+    """Width 256 (config 4's grid): column quads (default) == per-state LDS
+    layout == per-sweep shape, bit for bit, backward and a capped forward, two
+    instances."""
+    from irlmx import DeviceMDP, ops
+    size, B = 256, 2
+    n = size * size
+    mdp = DeviceMDP.icy_gridworld(size, [0.15, 0.3], device=dev)
+    rng = np.random.default_rng(8)
+    r = rng.uniform(0.0, 1.0, (B, n))
+    tm = ops.terminal_mask([n - 1], n, batch=B, device=dev)
+    p0 = np.zeros((B, n))
+    p0[:, 0] = 1.0
+    keys = ("IRLMX_FUSED_MAX_STATES", "IRLMX_CLUSTER", "IRLMX_CLUSTER_R", "IRLMX_CLUSTER_G", "IRLMX_PAIR")
+    out = {}
+    for name, env in (("sweep", {"IRLMX_CLUSTER": "0"}), ("lds", {"IRLMX_PAIR": "0"}), ("quads", {}),
+                      ("quads_small", {"IRLMX_CLUSTER_R": "5", "IRLMX_CLUSTER_G": "3"})):
+        for k in keys:
+            monkeypatch.delenv(k, raising=False)
+        for k, v in env.items():
+            monkeypatch.setenv(k, v)
+        pi = ops.backward_maxent(mdp, r, tm)
+        svf, k, st = ops.forward_svf(mdp, p0, tm, pi, max_iter=2500)
+        out[name] = (pi, svf, k)
+    for k in keys:
+        monkeypatch.delenv(k, raising=False)
+    for name in ("lds", "quads", "quads_small"):
+        assert torch.equal(out["sweep"][0], out[name][0]), (name, "pi")
+        assert torch.equal(out["sweep"][1], out[name][1]), (name, "svf")
+        assert torch.equal(out["sweep"][2], out[name][2]), (name, "sweeps")

@@ -14,7 +14,7 @@ tm = ops.terminal_mask([n - 1], n, batch=B, device=dev)
 r = torch.ones((B, n), dtype=torch.float64, device=dev)  # the reference's initial theta (Constant(1.0))
 p0 = torch.zeros((B, n), dtype=torch.float64, device=dev); p0[:, 0] = 1.0
 res = {}
-for pair, xg in (("0", "1"), ("1", "1"), ("2", "1")):
+for pair, xg in (("0", "1"), ("1", "1"), ("2", "1"), ("3", "1")):
     os.environ["IRLMX_PAIR"] = pair
     os.environ["IRLMX_XCD_GROUP"] = xg
     os.environ.pop("IRLMX_STAMPS", None)
@@ -32,6 +32,6 @@ for pair, xg in (("0", "1"), ("1", "1"), ("2", "1")):
     os.environ["IRLMX_STAMPS"] = "1"
     ops.backward_maxent(mdp, r, tm); torch.cuda.synchronize()
     os.environ.pop("IRLMX_STAMPS")
-for k in ("11", "21"):
+for k in ("11", "21", "31"):
     print("bit-identical", k, torch.equal(res["01"][0], res[k][0]), torch.equal(res["01"][1], res[k][1]),
           torch.equal(res["01"][2], res[k][2]))
