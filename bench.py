@@ -44,6 +44,12 @@ CONFIGS = {
 HBM_PEAK_GBS = 8000.0          # MI355X_MICROARCH.md: 8.0 TB/s spec
 BYTES_FWD = 168                # forward sweep, bytes per state per instance
 BYTES_BWD = 152                # backward sweep
+# fp64 arithmetic the sweeps execute per state: one FMA per
+# point of the collapsed 5-point stencil = 10 flop; the forward adds p0 (+1)
+FLOP_BWD = 10
+FLOP_FWD = 11
+FP64_PEAK_TFS = 78.6           # MI355X FP64 vector (= FP64 matrix) spec peak
+FP64_LOOP_TFS = 54.8           # tools/diag/dfma_rate.hip mode 0: independent fp64 FMA chains, 2 waves/SIMD
 
 
 def parse():
@@ -207,8 +213,10 @@ def main():
     # SURVEY 8(d) algorithmic bytes: per instance and sweep 152*S (backward), 168*S (forward)
     bwd_bytes = BYTES_BWD * S * float(2 * S) * per_gpu * args.steps
     fwd_bytes = BYTES_FWD * S * float(k_f.sum())
-    kern = {"backward": {"bytes": bwd_bytes, "seconds": t_bwd, "launches": args.steps},
-            "forward": {"bytes": fwd_bytes, "seconds": t_fwd, "launches": args.steps}}
+    kern = {"backward": {"bytes": bwd_bytes, "seconds": t_bwd, "launches": args.steps,
+                         "flop": FLOP_BWD * S * float(2 * S - 1) * per_gpu * args.steps},
+            "forward": {"bytes": fwd_bytes, "seconds": t_fwd, "launches": args.steps,
+                        "flop": FLOP_FWD * S * float(k_f.sum())}}
     dom = max(kern, key=lambda k: kern[k]["seconds"])
     achieved = kern[dom]["bytes"] / kern[dom]["seconds"] / 1e9
     if rank == 0:
@@ -241,8 +249,19 @@ def main():
                                  "instance-sweep) x sweeps / kernel time (HIP events on the launch stream); frac > 1: "
                                  "the state vectors and weights stay on chip across sweeps (LDS + registers), "
                                  "HBM only sees halo exchanges"},
+            "compute_roofline": {
+                "bound": "fp64-valu", "kernel": dom,
+                "achieved": kern[dom]["flop"] / kern[dom]["seconds"] / 1e12, "peak": FP64_PEAK_TFS,
+                "unit": "TFLOP/s", "frac": kern[dom]["flop"] / kern[dom]["seconds"] / 1e12 / FP64_PEAK_TFS,
+                "frac_of_fma_loop": kern[dom]["flop"] / kern[dom]["seconds"] / 1e12 / FP64_LOOP_TFS,
+                "flop_per_launch": kern[dom]["flop"] / kern[dom]["launches"],
+                "note": "the binding resource: every sweep is a chain of fp64 FMAs on the VALU (10 flop per "
+                        "state for the collapsed 5-point stencil, 11 forward); peak = MI355X FP64 spec, "
+                        "frac_of_fma_loop = vs a pure independent-FMA loop measured on the box "
+                        "(tools/diag/dfma_rate.hip, 54.8 TFLOP/s at the clock fp64 load holds)"},
             "per_kernel": {k: {"achieved_GBs": v["bytes"] / v["seconds"] / 1e9, "ms_per_launch": v["seconds"] /
-                               v["launches"] * 1e3} for k, v in kern.items()},
+                               v["launches"] * 1e3, "achieved_TFLOPs": v["flop"] / v["seconds"] / 1e12}
+                           for k, v in kern.items()},
         }
         tpath = args.traffic or _latest_traffic()
         if tpath and os.path.exists(tpath) and args.config == "c3" and not args.size and not args.batch:

@@ -336,9 +336,9 @@ __global__ void __launch_bounds__(NT) cluster_kernel(ClusterArgs a) {
           u[q] = make_double2(src[SPT - CPL + 2 * q], src[SPT - CPL + 2 * q + 1]);
         }
       }
-      __syncthreads();
       double above[CPL], below[CPL];  // bottom row of the band above, top row of the band below
-      {
+      auto edges_in = [&]() {
+        __syncthreads();
         const double2* t = bnd_at(i & 1, bb, 1);
         const double2* u = bnd_at(i & 1, bb + 2, 0);
 #pragma unroll
@@ -347,7 +347,7 @@ __global__ void __launch_bounds__(NT) cluster_kernel(ClusterArgs a) {
           above[2 * q] = x.x; above[2 * q + 1] = x.y;
           below[2 * q] = y.x; below[2 * q + 1] = y.y;
         }
-      }
+      };
       // rows j1 and j2 (j2 == j1: one row) at once: up to 2 * CPL independent FMA chains
       auto rows = [&](int j1, int j2) {
         const bool two = j2 != j1;
@@ -378,13 +378,21 @@ __global__ void __launch_bounds__(NT) cluster_kernel(ClusterArgs a) {
           }
         }
       };
-      // interior rows first (their operands are all in registers while the edge
-      // reads above are in flight), the band's bottom and top rows last; with
-      // two columns per lane, two rows at a time
+      // interior rows first (all their operands are registers), the band's
+      // bottom and top rows last; with two columns per lane, two rows at a
+      // time.  The first kPre interior steps run between the edge-row stores
+      // and the barrier (they hide the stores' completion and the other waves'
+      // arrival), the rest while the edge reads after the barrier are in flight.
       constexpr int step = CPL == 2 ? 2 : 1;
+      constexpr int n_int = RW >= 3 ? (RW - 2 + step - 1) / step : 0;
+      constexpr int kPre = (n_int + 1) / 2;
 #pragma unroll
-      for (int jp = 1; jp + step - 1 <= RW - 2; jp += step) rows(jp, jp + step - 1);
-      if constexpr (step == 2 && RW >= 3 && (RW - 2) % 2 == 1) rows(RW - 2, RW - 2);
+      for (int s = 0; s < n_int; ++s) {
+        if (s == kPre) edges_in();
+        const int jp = 1 + s * step;
+        rows(jp, jp + step - 1 <= RW - 2 ? jp + step - 1 : jp);
+      }
+      if constexpr (kPre >= n_int) edges_in();
       if constexpr (RW >= 2) {
         if constexpr (CPL == 2) rows(RW - 1, 0);
         else { rows(RW - 1, RW - 1); rows(0, 0); }
@@ -744,7 +752,6 @@ bool cluster_plan(int W, int H, int B, int mode, ClusterPlan* out) {
   const int cus = device_cus();
   if (cus <= 0) return false;
   const int fR = env_int("IRLMX_CLUSTER_R", 0), fG = env_int("IRLMX_CLUSTER_G", 0);
-  // layout for widths 64 / 128: IRLMX_PAIR = 2 (default) column strips, 1 pair rows, 0 per state
   // in-tile layout (IRLMX_PAIR forces one): widths 64 / 128 column pairs (2;
   // 1 = pair rows, 3 = column quads at 128), width 256 backward column quads
   // (3), other widths per state (0)
@@ -771,19 +778,23 @@ bool cluster_plan(int W, int H, int B, int mode, ClusterPlan* out) {
       int spt = (E + nt - 1) / nt;
       if (pair) spt = (spt + (layout == 3 ? 3 : 1)) / (layout == 3 ? 4 : 2) * (layout == 3 ? 4 : 2);
       if (spt > spt_max) continue;
-      if (cluster_lds(spt * nt, W, layout, nt, mode) > kMaxLdsBytes) continue;
+      const size_t lds = cluster_lds(spt * nt, W, layout, nt, mode);
+      if (lds > kMaxLdsBytes) continue;
       const int per = cus / C;
       if (per < 1) continue;
       const int nl = (B + per - 1) / per;
       // cycles per sweep (measured on MI355X, tools/diag/pair_bench.py): ~110 per
       // state slot per sweep, plus one halo exchange per block of G sweeps,
-      // ~5k cycles inside one L2, ~11k across XCDs
+      // ~5k cycles inside one L2, ~11k across XCDs.  (Two 256-thread
+      // workgroups per CU, each exchanging while the other sweeps, measured
+      // 1.5x slower at config 3: the exchange of a half-size tile costs as much
+      // as a full one and the two workgroups stay in phase.)
       const double xchg = xcd_groupable(std::min(per, B), C) ? 5000.0 : 11000.0;
       const double cost = nl * (110.0 * spt * G + xchg) / G;
       if (cost < best - 1e-9) {
         best = cost;
         ok = true;
-        *out = ClusterPlan{R, G, C, G, std::min(per, B), spt, spt * nt, cluster_lds(spt * nt, W, layout, nt, mode), layout, nt};
+        *out = ClusterPlan{R, G, C, G, std::min(per, B), spt, spt * nt, lds, layout, nt};
       }
     }
   }

@@ -1,0 +1,84 @@
+"""HIP path at the BASELINE configs' full grid sizes (needs an MI355X).
+
+128x128 (configs 3 and 5): the device's backward pass (2*S = 32,768 sweeps on
+the default cluster plan -- column-strip layout, 4 tiles per instance, halo
+exchanges, block-boundary rescaling) and a forward pass capped at 3,000
+sweeps, against the CPU oracle's sparse-operand restatement of the same
+reference statements (oracle/maxent_oracle.py ``*_csr``, maxent.py:98-112,
+143-159), two instances with distinct slip probabilities.  The reference
+itself overflows to NaN beyond 12x12 (its unscaled backward), so the oracle
+here is the rescaled restatement, pinned to the reference at small sizes
+(tests/test_oracle_golden.py).
+
+256x256 (config 4): size-independent properties of the backward (policy rows
+are distributions; instance order does not change any instance's result) --
+the CPU restatement would take minutes there.  Layout bit-identity at 256 is
+in test_gpu_parity.py::test_width256_quads_bit_identical.
+"""
+
+import numpy as np
+import pytest
+
+import maxent_oracle as O
+
+pytestmark = pytest.mark.gpu
+
+torch = pytest.importorskip("torch")
+
+RTOL = 1e-9       # device vs oracle (float64 both; different summation order only)
+CONTRACT = 1e-5   # north-star tolerance
+
+
+def rel_err(got, ref):
+    return float(np.max(np.abs(got - ref)) / np.max(np.abs(ref)))
+
+
+@pytest.fixture(scope="module")
+def dev():
+    import __graft_entry__ as g
+    g.build()
+    import irlmx
+    return irlmx.require_device()
+
+
+def test_config3_grid_vs_sparse_oracle(dev):
+    from irlmx import DeviceMDP, ops
+    size, slips = 128, (0.1, 0.3)
+    n, B = size * size, len(slips)
+    rng = np.random.default_rng(128)
+    r = rng.uniform(0.0, 1.0, (B, n))
+    mdp = DeviceMDP.icy_gridworld(size, list(slips), device=dev)
+    tm = ops.terminal_mask([n - 1], n, batch=B, device=dev)
+    p0 = np.zeros((B, n))
+    p0[:, 0] = 1.0
+    pi = ops.backward_maxent(mdp, r, tm)
+    svf, k, st = ops.forward_svf(mdp, p0, tm, pi, max_iter=3000)
+    pi_h, svf_h = pi.cpu().numpy(), svf.cpu().numpy()
+    for b, slip in enumerate(slips):
+        mats = O.icy_gridworld_csr(size, slip)
+        pi_ref = O.backward_maxent_csr(mats, [n - 1], r[b])
+        e = rel_err(pi_h[b], pi_ref)
+        assert e <= CONTRACT and e <= RTOL, (b, "pi", e)
+        assert np.argmax(pi_h[b], axis=1).tolist() == np.argmax(pi_ref, axis=1).tolist()
+        # forward on the device's own policy: isolates the forward pass
+        svf_ref, k_ref = O.forward_svf_csr(mats, p0[b], [n - 1], pi_h[b], max_iter=3000)
+        assert int(k[b]) == k_ref == 3000 and int(st[b]) == 2  # capped: IRLMX_MAXITER
+        e = rel_err(svf_h[b], svf_ref)
+        assert e <= CONTRACT and e <= RTOL, (b, "svf", e)
+
+
+def test_config4_grid_properties(dev):
+    from irlmx import DeviceMDP, ops
+    size = 256
+    n = size * size
+    rng = np.random.default_rng(256)
+    slips = [0.1, 0.2, 0.3]
+    r = rng.uniform(0.0, 1.0, (3, n))
+    tm = ops.terminal_mask([n - 1], n, batch=3, device=dev)
+    pi = ops.backward_maxent(DeviceMDP.icy_gridworld(size, slips, device=dev), r, tm).cpu().numpy()
+    assert np.all(np.isfinite(pi)) and np.all(pi >= 0.0)
+    assert np.max(np.abs(pi.sum(axis=2) - 1.0)) < 1e-12
+    # instances are independent: reversing the batch reverses the results, bit for bit
+    tm_r = ops.terminal_mask([n - 1], n, batch=3, device=dev)
+    pi_r = ops.backward_maxent(DeviceMDP.icy_gridworld(size, slips[::-1], device=dev), r[::-1].copy(), tm_r)
+    assert np.array_equal(pi_r.cpu().numpy()[::-1], pi)

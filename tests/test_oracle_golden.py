@@ -148,3 +148,27 @@ def test_causal_small_cases():
     P = O.icy_gridworld_table(5, 0.2)
     pi, _, ks = O.soft_backward(P, z["phi_vec__phi"], np.ones(25), 0.8)
     assert np.array_equal(pi, z["phi_vec__pi"]) and ks == int(z["phi_vec__k_s"])
+
+
+def test_sparse_oracle_matches_dense():
+    """The sparse-operand restatement (used at 128x128 in test_gpu_full_size.py)
+    builds the same table values as the dense oracle (bit for bit) and runs the
+    same statements: backward and forward agree to rounding, sweep counts equal."""
+    for size, slip in ((5, 0.2), (9, 0.1), (16, 0.3)):
+        P = O.icy_gridworld_table(size, slip)
+        mats = O.icy_gridworld_csr(size, slip)
+        assert np.array_equal(np.stack([m.toarray() for m in mats], axis=2), P), size
+    rng = np.random.default_rng(3)
+    for size in (5, 12):
+        n = size * size
+        P = O.icy_gridworld_table(size, 0.2)
+        mats = O.icy_gridworld_csr(size, 0.2)
+        r = rng.uniform(0.0, 1.0, n)
+        pi = O.backward_maxent(P, [n - 1], r, rescale=True)
+        pi_s = O.backward_maxent_csr(mats, [n - 1], r)
+        assert np.max(np.abs(pi_s - pi)) <= 1e-13 * np.max(pi)
+        p0 = np.zeros(n)
+        p0[0] = 1.0
+        d, k = O.forward_svf(P, p0, [n - 1], pi)
+        d_s, k_s = O.forward_svf_csr(mats, p0, [n - 1], pi)
+        assert k == k_s and np.max(np.abs(d_s - d)) <= 1e-12 * np.max(d)
