@@ -32,7 +32,9 @@ for v in variants:
     same = None if ref is None else bool(torch.equal(ref, pi))
     if ref is None:
         ref = pi
-    print(f"[{v or 'default'}] backward {min(ts) * 1e3:.2f} ms  bit-identical to first: {same}", flush=True)
+    import hashlib
+    h = hashlib.sha256(pi.cpu().numpy().tobytes()).hexdigest()[:16]
+    print(f"[{v or 'default'}] backward {min(ts) * 1e3:.2f} ms  bit-identical to first: {same}  sha {h}", flush=True)
     os.environ["IRLMX_STAMPS"] = "1"
     ops.backward_maxent(mdp, r, tm); torch.cuda.synchronize()
     os.environ.pop("IRLMX_STAMPS")
