@@ -12,7 +12,7 @@ constexpr int kCT = 1024;          // threads per workgroup, per-state layout
 constexpr int kSptMax = 6;         // states per thread, per-state layout (no VGPR spills at 128 VGPRs)
 constexpr int kPairThreads = 512;  // threads per workgroup, pair layouts (256 VGPRs)
 constexpr int kSptMaxPair = 12;    // states per thread, pair layouts -> extended tile <= 6144 states
-constexpr int kSptMaxQuadFwd = 8;  // forward with column quads (register budget)
+constexpr int kSptMaxQuadFwd = 12;  // forward with column quads (register budget)
 constexpr int kTMax = 16;          // max sweeps per block (= max ghost rows)
 constexpr size_t kMaxLdsBytes = 160 * 1024;  // LDS per CU (one workgroup per CU)
 constexpr int kModeFwd = 0;
@@ -141,6 +141,10 @@ __device__ inline unsigned long long wave_or_u64(unsigned long long v) {
   for (int off = 32; off > 0; off >>= 1) v |= __shfl_xor(v, off, kWave);
   return v;
 }
+
+// cluster_run's result when a forward instance turned non-finite: the call must
+// be rerun on the per-sweep shape (exact NaN bookkeeping; cluster.hip)
+constexpr int kClusterNonFinite = 1;
 
 bool cluster_plan(int W, int H, int B, int mode, ClusterPlan* out);
 int cluster_run(int mode, const ClusterPlan& p, ClusterArgs a, int B, hipStream_t st);

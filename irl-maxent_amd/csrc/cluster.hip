@@ -250,22 +250,27 @@ __global__ void __launch_bounds__(NT) cluster_kernel(ClusterArgs a) {
   __syncthreads();
 
   const double eps = a.eps;
-  // One Jacobi sweep over the extended tile.  Forward: sets bit i / 16 + i of
-  // `flags` for an owned |delta| > eps / NaN.  (Backward: the owned maximum for
+  // Forward convergence bookkeeping per sweep i of a block: bit i of `flags`
+  // = "the running fmax of this lane's owned |delta| exceeds eps" (two VALU
+  // instructions per state).  The reference stops at the first sweep whose
+  // np.max(|delta|) is not > eps, NaN included; fmax drops NaN, so the bits
+  // are exact unless some |delta| is NaN.  A non-finite value is sticky (every
+  // sweep multiplies a state's own value by its self weight, and 0 * inf =
+  // NaN), so a non-finite owned value at the block's end (bit 31, checked once
+  // per block) covers that case: the instance is then handed back to the host,
+  // which reruns the call on the per-sweep shape with exact NaN bookkeeping
+  // (bit-identical arithmetic; fixed_point.hip irlmx_forward_svf).
+  // One Jacobi sweep over the extended tile.  (Backward: the owned maximum for
   // the block-end rescale is taken once after the block's last sweep.)
   // Every slot l < SPT * NT is swept, also l >= E: those have zero weights and
   // zero c0, read only zeros (buffers are zero-filled and hold emax + 2 pads),
   // and stay 0 -- which is what state E - 1's down-neighbour must read.  No
   // per-state branch, so all LDS reads of a sweep can be in flight together.
-  auto sweep = [&](const double* __restrict__ din, double* __restrict__ dout, int i, unsigned& flags,
-                   int) {
+  auto sweep = [&](const double* __restrict__ din, double* __restrict__ dout, int i, unsigned& flags) {
     const unsigned ob = slot_bits(own_bits);
+    double dmax = 0.0;
     auto account = [&](int j, double nv, double self) {
-      if (MODE == kModeFwd && ((ob >> j) & 1u)) {
-        const double d = fabs(nv - self);
-        flags |= ((d > eps) ? 1u : 0u) << i;
-        flags |= ((d != d) ? 1u : 0u) << (16 + i);
-      }
+      if (MODE == kModeFwd && ((ob >> j) & 1u)) dmax = fmax(dmax, fabs(nv - self));
     };
     if constexpr (PAIR && !COLS) {
 #pragma unroll
@@ -312,6 +317,7 @@ __global__ void __launch_bounds__(NT) cluster_kernel(ClusterArgs a) {
         account(j, nv, self);
       }
     }
+    if (MODE == kModeFwd) flags |= ((dmax > eps) ? 1u : 0u) << i;
     __syncthreads();
   };
 
@@ -326,12 +332,9 @@ __global__ void __launch_bounds__(NT) cluster_kernel(ClusterArgs a) {
                         unsigned& flags) {
     if constexpr (COLS) {
       const unsigned ob = slot_bits(own_bits);
+      double dmax = 0.0;
       auto account = [&](int j, double nv, double self) {
-        if (MODE == kModeFwd && ((ob >> j) & 1u)) {
-          const double d = fabs(nv - self);
-          flags |= ((d > eps) ? 1u : 0u) << i;
-          flags |= ((d != d) ? 1u : 0u) << (16 + i);
-        }
+        if (MODE == kModeFwd && ((ob >> j) & 1u)) dmax = fmax(dmax, fabs(nv - self));
       };
       {  // band edge rows (old values) out
         double2* t = bnd_at(i & 1, bb + 1, 0);
@@ -341,6 +344,16 @@ __global__ void __launch_bounds__(NT) cluster_kernel(ClusterArgs a) {
           t[q] = make_double2(src[2 * q], src[2 * q + 1]);
           u[q] = make_double2(src[SPT - CPL + 2 * q], src[SPT - CPL + 2 * q + 1]);
         }
+      }
+      if (MODE == kModeFwd && i == 0) {
+        // forward: the block-start state into the LDS snapshot (for a stop inside
+        // the block), here rather than at the block boundary so that the stores
+        // overlap the first sweep's arithmetic
+        const unsigned xb = slot_bits(ext_bits);
+#pragma unroll
+        for (int jp = 0; jp < SPT / 2; ++jp)
+          if ((xb >> (2 * jp)) & 1u)
+            *reinterpret_cast<double2*>(snap + slot_state(2 * jp)) = make_double2(src[2 * jp], src[2 * jp + 1]);
       }
       double above[CPL], below[CPL];  // bottom row of the band above, top row of the band below
       // The band's own top / bottom rows are in the edge array too, so their
@@ -422,6 +435,7 @@ __global__ void __launch_bounds__(NT) cluster_kernel(ClusterArgs a) {
       } else {
         rows(0, 0);
       }
+      if (MODE == kModeFwd) flags |= ((dmax > eps) ? 1u : 0u) << i;
     }
   };
 
@@ -478,6 +492,32 @@ __global__ void __launch_bounds__(NT) cluster_kernel(ClusterArgs a) {
     }
   };
   const long long total = MODE == kModeBwd ? a.n_sweeps : -1;
+  // n sweeps from the current state (registers for PAIR layouts, else `cur`)
+  auto run_sweeps = [&](int n, unsigned& fl) {
+    if constexpr (COLS) {
+      int i = 0;
+      for (; i + 1 < n; i += 2) {
+        cols_sweep(cv, cw, i, fl);
+        cols_sweep(cw, cv, i + 1, fl);
+      }
+      if (i < n) {
+        cols_sweep(cv, cw, i, fl);
+#pragma unroll
+        for (int j = 0; j < (COLS ? SPT : 1); ++j) cv[j] = cw[j];
+      }
+    } else {
+      for (int i = 0; i < n; ++i) {
+        sweep(cur, oth, i, fl);
+        double* t = cur; cur = oth; oth = t;
+      }
+    }
+  };
+  // back to the block-start state (forward: the LDS snapshot)
+  auto restore = [&]() {
+    for (int l = tid; l < E; l += NT) cur[pad + l] = snap[l];
+    __syncthreads();
+    reload(cur);
+  };
   for (int m = 0;; ++m) {
     int Tm = T;
     if (MODE == kModeBwd) Tm = (int)min<long long>((long long)T, total - done);
@@ -497,10 +537,15 @@ __global__ void __launch_bounds__(NT) cluster_kernel(ClusterArgs a) {
       }
       __syncthreads();  // the last sweep's boundary reads are done
     } else {
-      for (int i = 0; i < Tm; ++i) {
-        sweep(cur, oth, i, flags, 0);
-        double* t = cur; cur = oth; oth = t;
-      }
+      run_sweeps(Tm, flags);
+    }
+    if (MODE == kModeFwd) {  // non-finite owned value at the block end: bit 31 (see above)
+      const unsigned ob = slot_bits(own_bits);
+      bool nf = false;
+#pragma unroll
+      for (int j = 0; j < SPT; ++j)
+        if ((ob >> j) & 1u) nf |= !isfinite(PAIR ? cv[PAIR ? j : 0] : cur[pad + slot_state(j)]);
+      if (nf) flags |= 1u << 31;
     }
     if (MODE == kModeBwd && a.rescale) {  // owned maximum of the block's last sweep
       const unsigned ob = slot_bits(own_bits);
@@ -546,7 +591,7 @@ __global__ void __launch_bounds__(NT) cluster_kernel(ClusterArgs a) {
     unsigned* red32 = (unsigned*)red;  // [0..1]: tile summary by parity, [2..3]: instance summary
     if (tid == 0) red32[2 + ((m + 1) & 1)] = 0u;  // last read in block m - 1
     if (MODE == kModeFwd) {
-      const unsigned wf = wave_reduce_u32<1>(flags) & (((1u << Tm) - 1) | (((1u << Tm) - 1) << 16));
+      const unsigned wf = wave_reduce_u32<1>(flags) & (((1u << Tm) - 1) | (1u << 31));
       if ((tid & (kWave - 1)) == 0 && wf) atomicOr(&red32[m & 1], wf);
     } else if (a.rescale) {
       const unsigned wc = wave_reduce_u32<0>(scale_code(bits_double(mx)));
@@ -561,67 +606,61 @@ __global__ void __launch_bounds__(NT) cluster_kernel(ClusterArgs a) {
     // ---- all polls of a thread in flight together: one round trip --------------
     bool ok = true;
     constexpr int GPT = PAIR ? kGatherPerThread : 1;  // ghost granules in flight per thread
-    for (int k0 = 0; k0 < max(ng, 1); k0 += GPT * NT) {
-      unsigned off[GPT + 1];
-      int ls[GPT];
-      unsigned want = 0;
+    auto gather = [&]() {
+      for (int k0 = 0; k0 < max(ng, 1); k0 += GPT * NT) {
+        unsigned off[GPT + 1];
+        int ls[GPT];
+        unsigned want = 0;
 #pragma unroll
-      for (int i = 0; i < GPT; ++i) {
-        const int k = k0 + tid + i * NT;
-        ls[i] = k < ng0 ? k : own1 + (k - ng0);
-        off[i] = (gpar + (unsigned)(base + ls[i])) * 16u;
-        want |= (k < ng ? 1u : 0u) << i;
-      }
-      off[GPT] = ((unsigned)(m & 1) * (unsigned)a.H + (unsigned)tid) * 16u;
-      want |= (k0 == 0 && tid < a.C ? 1u : 0u) << GPT;
-      unsigned long long v[GPT + 1];
-      ok &= gran_gather<GPT + 1>(rg, rs, off, want, tag, v);
+        for (int i = 0; i < GPT; ++i) {
+          const int k = k0 + tid + i * NT;
+          ls[i] = k < ng0 ? k : own1 + (k - ng0);
+          off[i] = (gpar + (unsigned)(base + ls[i])) * 16u;
+          want |= (k < ng ? 1u : 0u) << i;
+        }
+        off[GPT] = ((unsigned)(m & 1) * (unsigned)a.H + (unsigned)tid) * 16u;
+        want |= (k0 == 0 && tid < a.C ? 1u : 0u) << GPT;
+        unsigned long long v[GPT + 1];
+        ok &= gran_gather<GPT + 1>(rg, rs, off, want, tag, v);
 #pragma unroll
-      for (int i = 0; i < GPT; ++i)
-        if ((want >> i) & 1u) cur[pad + ls[i]] = bits_double(v[i]);
-      if ((want >> GPT) & 1u) {
-        if (MODE == kModeFwd) atomicOr(&red32[2 + (m & 1)], (unsigned)v[GPT]);
-        else atomicMax(&red32[2 + (m & 1)], (unsigned)v[GPT]);
+        for (int i = 0; i < GPT; ++i)
+          if ((want >> i) & 1u) cur[pad + ls[i]] = bits_double(v[i]);
+        if ((want >> GPT) & 1u) {
+          if (MODE == kModeFwd) atomicOr(&red32[2 + (m & 1)], (unsigned)v[GPT]);
+          else atomicMax(&red32[2 + (m & 1)], (unsigned)v[GPT]);
+        }
       }
-    }
+    };
+    gather();
     if (!ok) { lflag[0] = 1; atomicOr(a.err, 1); }
     __syncthreads();
     if (lflag[0]) return;  // exchange timed out (reported through a.err)
-    const unsigned summary = red32[2 + (m & 1)];
+    const unsigned summary =
+        MODE == kModeFwd ? (unsigned)__builtin_amdgcn_readfirstlane((int)red32[2 + (m & 1)]) : red32[2 + (m & 1)];
     if (tid == 0) red32[m & 1] = 0u;  // next-but-one block's tile summary (read above)
     stamp(2);
     if (MODE == kModeFwd) {
       const unsigned msk = summary;
+      if (msk >> 31) {
+        // a non-finite value: every tile of the instance sees the same bit and
+        // leaves; the host reruns the call with exact NaN bookkeeping
+        stamp_flush();
+        if (tile == 0 && tid == 0) atomicOr(a.err, 2);
+        return;
+      }
       int conv = 0;
-      bool nan_stop = false;
-      for (int i = 0; i < Tm; ++i) {
-        const bool cap = a.max_iter > 0 && done + i + 1 >= a.max_iter;
-        nan_stop = (msk >> (16 + i)) & 1u;
-        if (nan_stop || !((msk >> i) & 1u) || cap) { conv = i + 1; break; }
+      const unsigned live = (1u << Tm) - 1;
+      if ((msk & live) != live || (a.max_iter > 0 && done + Tm >= a.max_iter)) {
+        for (int i = 0; i < Tm; ++i) {
+          const bool cap = a.max_iter > 0 && done + i + 1 >= a.max_iter;
+          if (!((msk >> i) & 1u) || cap) { conv = i + 1; break; }
+        }
       }
       if (conv) {
         // exact stop inside the block: replay `conv` sweeps from the block-start state
-        for (int l = tid; l < E; l += NT) cur[pad + l] = snap[l];
-        __syncthreads();
-        reload(cur);
+        restore();
         unsigned scratch = 0;
-        if constexpr (COLS) {
-          int i = 0;
-          for (; i + 1 < conv; i += 2) {
-            cols_sweep(cv, cw, i, scratch);
-            cols_sweep(cw, cv, i + 1, scratch);
-          }
-          if (i < conv) {
-            cols_sweep(cv, cw, i, scratch);
-#pragma unroll
-            for (int j = 0; j < (COLS ? SPT : 1); ++j) cv[j] = cw[j];
-          }
-        } else {
-          for (int i = 0; i < conv; ++i) {
-            sweep(cur, oth, i, scratch, 0);
-            double* t = cur; cur = oth; oth = t;
-          }
-        }
+        run_sweeps(conv, scratch);
         if (COLS) {
           const unsigned ob = slot_bits(own_bits);
 #pragma unroll
@@ -635,7 +674,7 @@ __global__ void __launch_bounds__(NT) cluster_kernel(ClusterArgs a) {
         if (tile == 0 && tid == 0) {
           const bool big = (msk >> (conv - 1)) & 1u;
           a.iters[inst] = done + conv;
-          a.status[inst] = nan_stop ? IRLMX_NONFINITE : (big ? IRLMX_MAXITER : IRLMX_OK);
+          a.status[inst] = big ? IRLMX_MAXITER : IRLMX_OK;
         }
         return;
       }
@@ -656,7 +695,7 @@ __global__ void __launch_bounds__(NT) cluster_kernel(ClusterArgs a) {
           v.y = ldexp(v.y, e_scale);
           if (ext && !COLS) *reinterpret_cast<double2*>(cur + pad + l) = v;
         }
-        if (MODE == kModeFwd && ext) *reinterpret_cast<double2*>(snap + l) = v;
+        if (MODE == kModeFwd && ext && !COLS) *reinterpret_cast<double2*>(snap + l) = v;  // COLS: in the first sweep
         cv[PAIR ? 2 * jp : 0] = v.x;
         cv[PAIR ? 2 * jp + 1 : 0] = v.y;
       }
@@ -857,7 +896,7 @@ static void* cluster_fn_quad(int spt) {
   switch (spt) {
     case 4: return (void*)&cluster_kernel<MODE, 4, WT, 3, kPairThreads>;
     case 8: return (void*)&cluster_kernel<MODE, 8, WT, 3, kPairThreads>;
-    case 12: return MODE == kModeBwd ? (void*)&cluster_kernel<MODE, 12, WT, 3, kPairThreads> : nullptr;
+    case 12: return (void*)&cluster_kernel<MODE, 12, WT, 3, kPairThreads>;
   }
   return nullptr;
 }
@@ -886,14 +925,6 @@ static void* cluster_fn(int spt, int W, int layout, int) {
 // check the exchange-timeout word (synchronises the stream).
 int cluster_run(int mode, const ClusterPlan& plan, ClusterArgs a, int B, hipStream_t st) {
   ClusterPlan p = plan;
-  if (mode == kModeFwd && p.pair == 2 && p.spt > 6) {
-    // the forward's convergence bookkeeping does not fit the column-strip kernel's
-    // registers at this depth: same tiles, pair-row layout
-    p.pair = 1;
-    p.nt = kPairThreads;
-    p.spt = p.emax / kPairThreads;
-    p.lds = cluster_lds(p.emax, a.W, 1, p.nt, mode);
-  }
   void* fn;
   fn = mode == kModeFwd ? cluster_fn<kModeFwd>(p.spt, a.W, p.pair, p.nt) : cluster_fn<kModeBwd>(p.spt, a.W, p.pair, p.nt);
   const int nt = p.nt;
@@ -945,8 +976,8 @@ int cluster_run(int mode, const ClusterPlan& plan, ClusterArgs a, int B, hipStre
     free(h);
     hipFree(stamps);
   }
-  if (err) { set_error("cluster: halo exchange timed out (workgroups not co-resident?)"); return IRLMX_EHIP; }
-  return 0;
+  if (err & 1) { set_error("cluster: halo exchange timed out (workgroups not co-resident?)"); return IRLMX_EHIP; }
+  return (err & 2) ? kClusterNonFinite : 0;
 }
 
 }  // namespace irlmx

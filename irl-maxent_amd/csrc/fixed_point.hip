@@ -926,7 +926,14 @@ extern "C" int irlmx_forward_svf(const irlmx_mdp* mdp, const double* p_initial, 
     ca.eps = eps; ca.max_iter = (long long)max_iter;
     ca.gran = ws.gran; ca.sgran = ws.sgran; ca.err = ws.err;
     ca.out = svf; ca.iters = iterations; ca.status = status;
-    return cluster_run(kModeFwd, cp, ca, m.B, st);
+    const int rc = cluster_run(kModeFwd, cp, ca, m.B, st);
+    if (rc != kClusterNonFinite) return rc;
+    // an instance turned non-finite (rare): the cluster shape's convergence bits
+    // drop NaN deltas, so rerun the call on the per-sweep shape, whose
+    // bookkeeping is exact (same arithmetic, bit-identical results)
+    e = hipMemsetAsync(workspace, 0, ws.total, st);
+    if (e != hipSuccess) return hip_fail(e, "workspace memset");
+    hipLaunchKernelGGL(fwd_weights_kernel, g, dim3(256), 0, st, m, p_action, terminal, ws.wgt, ws.bad);
   }
   const dim3 gs((m.S + kSweepThreads - 1) / kSweepThreads, m.B);
   int rc = run_until_done(ws, m.B, st, [&](long long it, int r3) {
