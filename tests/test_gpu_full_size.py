@@ -82,3 +82,32 @@ def test_config4_grid_properties(dev):
     tm_r = ops.terminal_mask([n - 1], n, batch=3, device=dev)
     pi_r = ops.backward_maxent(DeviceMDP.icy_gridworld(size, slips[::-1], device=dev), r[::-1].copy(), tm_r)
     assert np.array_equal(pi_r.cpu().numpy()[::-1], pi)
+
+
+@pytest.mark.parametrize("bad", [np.inf, np.nan])
+def test_cluster_forward_nonfinite_rerun(dev, bad, monkeypatch):
+    """A non-finite start distribution on the cluster shape (64x64, column pairs):
+    the block-end check hands the call to the per-sweep shape, whose exact NaN
+    bookkeeping stops where the reference's loop does (inf: |inf - inf| = NaN one
+    sweep later; NaN: at once).  Asserted: the reference's sweep count (dense
+    oracle statements on CSR operands), status NONFINITE, and results bit for bit
+    those of the per-sweep shape run directly.  (Values after a NaN stop are not
+    compared with the reference: its dense product spreads NaN to every state.)"""
+    from irlmx import DeviceMDP, ops
+    size = 64
+    n = size * size
+    mdp = DeviceMDP.icy_gridworld(size, 0.2, device=dev)
+    tm = ops.terminal_mask([n - 1], n, device=dev)
+    r = np.random.default_rng(64).uniform(0.0, 1.0, n)
+    pi = ops.backward_maxent(mdp, r, tm)
+    p0 = np.zeros(n)
+    p0[0] = 0.5
+    p0[777] = bad
+    svf, k, st = ops.forward_svf(mdp, p0, tm, pi)
+    _, k_ref = O.forward_svf_csr(O.icy_gridworld_csr(size, 0.2), p0, [n - 1], pi[0].cpu().numpy())
+    assert int(k[0]) == k_ref == (2 if np.isinf(bad) else 1) and int(st[0]) == 1  # IRLMX_NONFINITE
+    monkeypatch.setenv("IRLMX_CLUSTER", "0")
+    monkeypatch.setenv("IRLMX_FUSED_MAX_STATES", "0")
+    svf_s, k_s, st_s = ops.forward_svf(mdp, p0, tm, pi)
+    assert torch.equal(svf_s.view(torch.int64), svf.view(torch.int64))  # bit patterns (NaN included)
+    assert torch.equal(k_s, k) and torch.equal(st_s, st)
