@@ -14,6 +14,7 @@ constexpr int kPairThreads = 512;  // threads per workgroup, pair layouts (256 V
 constexpr int kSptMaxPair = 12;    // states per thread, pair layouts -> extended tile <= 6144 states
 constexpr int kSptMaxQuadFwd = 12;  // forward with column quads (register budget)
 constexpr int kTMax = 16;          // max sweeps per block (= max ghost rows)
+constexpr int kRescaleEvery = 4;   // backward: max blocks between rescales
 constexpr size_t kMaxLdsBytes = 160 * 1024;  // LDS per CU (one workgroup per CU)
 constexpr int kModeFwd = 0;
 constexpr int kModeBwd = 1;

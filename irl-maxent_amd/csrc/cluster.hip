@@ -239,12 +239,19 @@ __global__ void __launch_bounds__(NT) cluster_kernel(ClusterArgs a) {
   };
 
   int T = a.T;
+  // Backward rescaling period: blocks between rescales (see the block loop).
+  // Growth over P_max blocks stays below 2^900 (g^(P_max T) < 2^900).
+  int p_max = 1;
   if (MODE == kModeBwd) {
     // cap the block so the growth over T sweeps stays below 2^900
     const double g = bits_double(a.growth[inst]);
-    if (a.rescale && g > 2.0 && isfinite(g)) {
-      const int cap = (int)floor(900.0 / log2(g)) - 1;
-      T = max(1, min(T, cap));
+    if (a.rescale && isfinite(g)) {
+      int cap = 1 << 20;
+      if (g > 2.0) {
+        cap = (int)floor(900.0 / log2(g)) - 1;
+        T = max(1, min(T, cap));
+      }
+      p_max = max(1, min(kRescaleEvery, cap / T));
     }
   }
   __syncthreads();
@@ -492,6 +499,7 @@ __global__ void __launch_bounds__(NT) cluster_kernel(ClusterArgs a) {
     }
   };
   const long long total = MODE == kModeBwd ? a.n_sweeps : -1;
+  int rescale_in = 1;  // backward: blocks until the next rescale
   // n sweeps from the current state (registers for PAIR layouts, else `cur`)
   auto run_sweeps = [&](int n, unsigned& fl) {
     if constexpr (COLS) {
@@ -523,7 +531,13 @@ __global__ void __launch_bounds__(NT) cluster_kernel(ClusterArgs a) {
     if (MODE == kModeBwd) Tm = (int)min<long long>((long long)T, total - done);
     // ---- T_m sweeps on chip ----------------------------------------------
     unsigned flags = 0;
-    unsigned long long mx = 0ull;
+    // Backward: rescale at the end of this block?  Every block until the
+    // partition vector is seen growing (a non-positive rescale exponent after
+    // the first blocks), then every p_max blocks, and always at the last block.
+    // Rescaling by a power of two is exact, so the period changes no result
+    // while values stay in range; blocks in between publish a zero code.
+    const bool resc = MODE == kModeBwd && a.rescale && (rescale_in <= 1 || done + Tm >= total);
+    double mxd = 0.0;
     if constexpr (COLS) {
       int i = 0;
       for (; i + 1 < Tm; i += 2) {
@@ -547,13 +561,11 @@ __global__ void __launch_bounds__(NT) cluster_kernel(ClusterArgs a) {
         if ((ob >> j) & 1u) nf |= !isfinite(PAIR ? cv[PAIR ? j : 0] : cur[pad + slot_state(j)]);
       if (nf) flags |= 1u << 31;
     }
-    if (MODE == kModeBwd && a.rescale) {  // owned maximum of the block's last sweep
+    if (resc) {  // owned maximum of the block's last sweep (fmax: a NaN is skipped, inf kept)
       const unsigned ob = slot_bits(own_bits);
 #pragma unroll
-      for (int j = 0; j < SPT; ++j) {
-        const unsigned long long d = abs_bits(PAIR ? cv[PAIR ? j : 0] : cur[pad + slot_state(j)]);
-        if (((ob >> j) & 1u) && d > mx) mx = d;
-      }
+      for (int j = 0; j < SPT; ++j)
+        if ((ob >> j) & 1u) mxd = fmax(mxd, fabs(PAIR ? cv[PAIR ? j : 0] : cur[pad + slot_state(j)]));
     }
     stamp(0);
     if (stamps) st_acc[4] += 1;
@@ -593,8 +605,8 @@ __global__ void __launch_bounds__(NT) cluster_kernel(ClusterArgs a) {
     if (MODE == kModeFwd) {
       const unsigned wf = wave_reduce_u32<1>(flags) & (((1u << Tm) - 1) | (1u << 31));
       if ((tid & (kWave - 1)) == 0 && wf) atomicOr(&red32[m & 1], wf);
-    } else if (a.rescale) {
-      const unsigned wc = wave_reduce_u32<0>(scale_code(bits_double(mx)));
+    } else if (resc) {
+      const unsigned wc = wave_reduce_u32<0>(scale_code(mxd));
       if ((tid & (kWave - 1)) == 0 && wc) atomicMax(&red32[m & 1], wc);
     }
     if (stamps) { const unsigned long long t = stamp_now(); st_acc[6] += t - ts; }
@@ -681,7 +693,8 @@ __global__ void __launch_bounds__(NT) cluster_kernel(ClusterArgs a) {
     }
     done += Tm;
     // ---- rescale (backward), snapshot (forward), register copy (pair) --------
-    const int e_scale = (MODE == kModeBwd && a.rescale) ? code_exponent(summary) : 0;
+    const int e_scale = resc ? code_exponent(summary) : 0;
+    if (MODE == kModeBwd) rescale_in = resc ? ((e_scale <= 0 && m >= 3) ? p_max : 1) : rescale_in - 1;
     if constexpr (PAIR) {
       const unsigned ob = slot_bits(own_bits), xb = slot_bits(ext_bits);
 #pragma unroll

@@ -17,6 +17,7 @@ mdp = DeviceMDP.icy_gridworld(size, np.linspace(0.1, 0.3, B), device=dev)
 tm = ops.terminal_mask([n - 1], n, batch=B, device=dev)
 r = torch.ones((B, n), dtype=torch.float64, device=dev)
 variants = sys.argv[1:] or [""]
+RESC = os.environ.get("RESCALE", "1") != "0"
 keys = ("IRLMX_NT", "IRLMX_PAIR", "IRLMX_CLUSTER_R", "IRLMX_CLUSTER_G", "IRLMX_STAMPS")
 ref = None
 for v in variants:
@@ -25,10 +26,10 @@ for v in variants:
     for kv in filter(None, v.split(",")):
         k, val = kv.split("=")
         os.environ[k] = val
-    pi = ops.backward_maxent(mdp, r, tm); torch.cuda.synchronize()
+    pi = ops.backward_maxent(mdp, r, tm, rescale=RESC); torch.cuda.synchronize()
     ts = []
     for _ in range(4):
-        t = time.perf_counter(); pi = ops.backward_maxent(mdp, r, tm); torch.cuda.synchronize(); ts.append(time.perf_counter() - t)
+        t = time.perf_counter(); pi = ops.backward_maxent(mdp, r, tm, rescale=RESC); torch.cuda.synchronize(); ts.append(time.perf_counter() - t)
     same = None if ref is None else bool(torch.equal(ref, pi))
     if ref is None:
         ref = pi
@@ -36,5 +37,5 @@ for v in variants:
     h = hashlib.sha256(pi.cpu().numpy().tobytes()).hexdigest()[:16]
     print(f"[{v or 'default'}] backward {min(ts) * 1e3:.2f} ms  bit-identical to first: {same}  sha {h}", flush=True)
     os.environ["IRLMX_STAMPS"] = "1"
-    ops.backward_maxent(mdp, r, tm); torch.cuda.synchronize()
+    ops.backward_maxent(mdp, r, tm, rescale=RESC); torch.cuda.synchronize()
     os.environ.pop("IRLMX_STAMPS")
