@@ -74,8 +74,23 @@ def _latest_traffic():
     return files[-1] if files else None
 
 
+CPU_DENSE_MAX = 128   # larger dense fp64 tables do not fit host RAM (256x256: 137 GB); extrapolate
+
+
 def cpu_baseline(size, p_slip, k_b, k_f, n_sweeps):
-    """Time the reference's dense statements on one instance (oracle restatement)."""
+    """Time the reference's dense statements on one instance (oracle restatement).
+
+    Above 128x128 the dense table does not fit in host memory: the statements are
+    timed at 128x128 and scaled by the dense work ratio (S / 16384)^2, labelled
+    "extrapolated" (SURVEY.md 8(d))."""
+    if size > CPU_DENSE_MAX:
+        base = cpu_baseline(CPU_DENSE_MAX, p_slip, k_b, k_f, n_sweeps)
+        ratio = (size * size / float(CPU_DENSE_MAX * CPU_DENSE_MAX)) ** 2
+        base["value"] /= ratio
+        base["sample"] = (f"extrapolated: {size}x{size} dense fp64 does not fit host RAM; per-sweep and copy "
+                          f"times measured at {CPU_DENSE_MAX}x{CPU_DENSE_MAX} x (S ratio)^2 = {ratio:.0f}, with "
+                          f"this run's K_b={k_b}, K_f={k_f:.0f} -- " + base["sample"])
+        return base
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import maxent_oracle as O
     try:
