@@ -572,6 +572,11 @@ __global__ void __launch_bounds__(NT) cluster_kernel(ClusterArgs a) {
     // ---- publish the halo rows, tagged with the block ------------------------
     const unsigned tag = salt | (((unsigned)m + 1u) & 0xFFFFFu);
     const unsigned gpar = (unsigned)(m & 1) * (unsigned)S;
+    // one tile per instance (C == 1: a 64x64 grid fits one CU): no halo, the
+    // block summary is the tile's own -- no hand-off at all.  (Compiled in for
+    // width 64 only: wider grids never fit one tile, and their kernels keep the
+    // exchange code exactly as scheduled without this branch.)
+    const bool solo = WT == 64 && a.C == 1;
     auto store_rows = [&]() {  // from the LDS tile, spread evenly over all threads
       for (int l = own0 + tid; l < pubA1; l += NT)
         gran_store(rg, (gpar + (unsigned)(base + l)) * 16u, dbits(cur[pad + l]), tag, plain);
@@ -611,8 +616,10 @@ __global__ void __launch_bounds__(NT) cluster_kernel(ClusterArgs a) {
     }
     if (stamps) { const unsigned long long t = stamp_now(); st_acc[6] += t - ts; }
     __syncthreads();  // the tile summary in red32[m & 1] (and COLS: the staged rows) complete
-    if (tid == 0) gran_store(rs, ((unsigned)(m & 1) * (unsigned)a.H + (unsigned)tile) * 16u, red32[m & 1], tag, plain);
-    if constexpr (COLS) store_rows();
+    if (!solo) {
+      if (tid == 0) gran_store(rs, ((unsigned)(m & 1) * (unsigned)a.H + (unsigned)tile) * 16u, red32[m & 1], tag, plain);
+      if constexpr (COLS) store_rows();
+    }
     stamp(1);
     // ---- gather this tile's ghost rows and (threads < C) every tile's summary,
     // ---- all polls of a thread in flight together: one round trip --------------
@@ -643,7 +650,8 @@ __global__ void __launch_bounds__(NT) cluster_kernel(ClusterArgs a) {
         }
       }
     };
-    gather();
+    if (!solo) gather();
+    else if (tid == 0) red32[2 + (m & 1)] = red32[m & 1];
     if (!ok) { lflag[0] = 1; atomicOr(a.err, 1); }
     __syncthreads();
     if (lflag[0]) return;  // exchange timed out (reported through a.err)
@@ -864,8 +872,12 @@ bool cluster_plan(int W, int H, int B, int mode, ClusterPlan* out) {
       // workgroups per CU, each exchanging while the other sweeps, measured
       // 1.5x slower at config 3: the exchange of a half-size tile costs as much
       // as a full one and the two workgroups stay in phase.)
-      const double xchg = xcd_groupable(std::min(per, B), C) ? 5000.0 : 11000.0;
-      const double cost = nl * (110.0 * spt * G + xchg) / G;
+      // (a single tile per instance needs no hand-off: ~0.8k cycles of block
+      // bookkeeping; a sweep takes at least ~850 cycles of barrier, LDS and
+      // FMA-chain latency however few states a lane holds)
+      const double xchg = (C == 1 && W == 64 && layout > 0) ? 800.0 : xcd_groupable(std::min(per, B), C) ? 5000.0 : 11000.0;
+      // (the forward's convergence bookkeeping: ~165 cycles per slot)
+      const double cost = nl * (std::max((mode == kModeFwd ? 165.0 : 110.0) * spt, 850.0) * G + xchg) / G;
       if (cost < best - 1e-9) {
         best = cost;
         ok = true;

@@ -446,7 +446,9 @@ def test_pair_layout_bit_identical(dev, monkeypatch):
               "rows": {"IRLMX_FUSED_MAX_STATES": "0", "IRLMX_PAIR": "1"},
               "quads": {"IRLMX_FUSED_MAX_STATES": "0", "IRLMX_PAIR": "3"},  # width 128 only (else column pairs)
               "pair": {"IRLMX_FUSED_MAX_STATES": "0"},
-              "pair_small": {"IRLMX_FUSED_MAX_STATES": "0", "IRLMX_CLUSTER_R": "7", "IRLMX_CLUSTER_G": "3"}}
+              "pair_small": {"IRLMX_FUSED_MAX_STATES": "0", "IRLMX_CLUSTER_R": "7", "IRLMX_CLUSTER_G": "3"},
+              # one tile per instance at width 64 (no hand-off; forward and backward)
+              "solo": {"IRLMX_FUSED_MAX_STATES": "0", "IRLMX_CLUSTER_R": "64", "IRLMX_CLUSTER_G": "16"}}
     rng = np.random.default_rng(5)
     for size, theta, cap in ((64, "ones", 20000), (64, "unif", 20000), (128, "unif", 3000)):
         n = size * size
@@ -466,7 +468,7 @@ def test_pair_layout_bit_identical(dev, monkeypatch):
             out[name] = (pi, svf, int(k[0]))
         for k in keys:
             monkeypatch.delenv(k, raising=False)
-        for name in ("no_cluster", "lds", "rows", "quads", "pair", "pair_small"):
+        for name in ("no_cluster", "lds", "rows", "quads", "pair", "pair_small", "solo"):
             assert torch.equal(out["sweep"][0], out[name][0]), (size, theta, name, "pi")
             assert torch.equal(out["sweep"][1], out[name][1]), (size, theta, name, "svf")
             assert out["sweep"][2] == out[name][2], (size, theta, name)
