@@ -174,6 +174,23 @@ int irlmx_build_gridworld(int32_t size, int32_t batch, double* row_val, void* st
 int irlmx_dense_to_stencil(const double* dense, int32_t width, int32_t height, int32_t n_actions,
                            double* row_val, int32_t* off_stencil, void* stream);
 
+/*
+ * Dense [S][S][A] float64 table (device) -> ELL layout (any sparsity), in two
+ * calls.  irlmx_dense_ell_sizes writes k_out[0] = max targets per source state
+ * (union over actions) and k_out[1] = max sources per target state (device
+ * int32[2]; col_count = device int32[S] scratch); the caller sizes the arrays
+ * with max(1, k) and calls irlmx_dense_to_ell:
+ *   row_idx [k_row][S], row_val [A][k_row][S]  targets of each state, ascending
+ *   col_idx [k_col][S], col_val [A][k_col][S]  sources of each state, ascending
+ * unused slots point at the state itself with value 0.  Replaces the host
+ * conversion of the reference's dense p_transition (maxent.py:98-102, 143) for
+ * non-grid models.
+ */
+int irlmx_dense_ell_sizes(const double* dense, int32_t n_states, int32_t n_actions, int32_t* k_out,
+                          int32_t* col_count, void* stream);
+int irlmx_dense_to_ell(const double* dense, int32_t n_states, int32_t n_actions, int32_t k_row, int32_t k_col,
+                       int32_t* row_idx, double* row_val, int32_t* col_idx, double* col_val, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -970,7 +970,7 @@ int cluster_run(int mode, const ClusterPlan& plan, ClusterArgs a, int B, hipStre
   if (env_int("IRLMX_STAMPS", 0)) {  // diagnostics only: phase cycle counters per workgroup
     e = hipMallocAsync((void**)&stamps, sizeof(unsigned long long) * 8 * nwg, st);
     if (e != hipSuccess) return hip_fail(e, "stamps alloc");
-    hipMemsetAsync(stamps, 0, sizeof(unsigned long long) * 8 * nwg, st);
+    (void)hipMemsetAsync(stamps, 0, sizeof(unsigned long long) * 8 * nwg, st);
   }
   a.stamps = stamps;
   for (int b0 = 0; b0 < B; b0 += p.per_launch) {
@@ -990,7 +990,7 @@ int cluster_run(int mode, const ClusterPlan& plan, ClusterArgs a, int B, hipStre
   if (e != hipSuccess) return hip_fail(e, "cluster sync");
   if (stamps) {
     unsigned long long* h = (unsigned long long*)malloc(sizeof(unsigned long long) * 8 * nwg);
-    hipMemcpy(h, stamps, sizeof(unsigned long long) * 8 * nwg, hipMemcpyDeviceToHost);
+    (void)hipMemcpy(h, stamps, sizeof(unsigned long long) * 8 * nwg, hipMemcpyDeviceToHost);
     double acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
     for (int g = 0; g < nwg; ++g)
       for (int k = 0; k < 8; ++k) acc[k] += (double)h[(size_t)g * 8 + k] / nwg;
@@ -999,7 +999,7 @@ int cluster_run(int mode, const ClusterPlan& plan, ClusterArgs a, int B, hipStre
             acc[4], acc[0] / acc[4], acc[1] / acc[4], acc[2] / acc[4], acc[3] / acc[4], acc[5], acc[6] / acc[4],
             (acc[7] - acc[6]) / acc[4]);
     free(h);
-    hipFree(stamps);
+    (void)hipFree(stamps);
   }
   if (err & 1) { set_error("cluster: halo exchange timed out (workgroups not co-resident?)"); return IRLMX_EHIP; }
   return (err & 2) ? kClusterNonFinite : 0;

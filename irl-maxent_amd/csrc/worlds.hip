@@ -198,3 +198,128 @@ extern "C" int irlmx_stochastic_policy(const int32_t* successor, int32_t n_state
   hipError_t e = hipGetLastError();
   return e == hipSuccess ? 0 : hip_fail(e, "stochastic_policy_kernel");
 }
+
+// ---------------------------------------------------------------------------
+// Dense [S][S][A] -> ELL row and column forms (any sparsity), on the device.
+// Replaces the host-side conversion a dense upload of a non-grid MDP needed
+// (maxent.py callers pass the reference's dense p_transition, maxent.py:98-102,
+// 143).  Layout (include/irlmx.h): row form = per source state the union over
+// actions of its targets, ascending; column form = per target the union of its
+// sources, ascending; unused slots point at the state itself with value 0.
+// ---------------------------------------------------------------------------
+
+namespace irlmx {
+
+// Does (s, t) carry a nonzero for some action?
+__device__ inline bool ell_nz(const double* __restrict__ dense, size_t S, int A, size_t s, size_t t) {
+  const double* p = dense + (s * S + t) * A;
+  bool nz = false;
+  for (int a = 0; a < A; ++a) nz |= p[a] != 0.0;
+  return nz;
+}
+
+// One wave per source row: union sizes per row (max into k[0]) and per-target
+// counts (col_count, summed over rows; its max is taken by ell_colmax_kernel).
+__global__ void ell_count_kernel(const double* __restrict__ dense, int S, int A, int32_t* __restrict__ k,
+                                 int32_t* __restrict__ col_count) {
+  const int lane = threadIdx.x & (kWave - 1);
+  const int s = blockIdx.x * (blockDim.x / kWave) + threadIdx.x / kWave;
+  if (s >= S) return;
+  int cnt = 0;
+  for (int t0 = 0; t0 < S; t0 += kWave) {
+    const int t = t0 + lane;
+    const bool nz = t < S && ell_nz(dense, (size_t)S, A, (size_t)s, (size_t)t);
+    if (nz) atomicAdd(&col_count[t], 1);
+    cnt += __popcll(__ballot(nz));
+  }
+  if (lane == 0) atomicMax(&k[0], cnt);
+}
+
+__global__ void ell_colmax_kernel(const int32_t* __restrict__ col_count, int S, int32_t* __restrict__ k) {
+  int m = 0;
+  for (int t = blockIdx.x * blockDim.x + threadIdx.x; t < S; t += gridDim.x * blockDim.x) m = max(m, col_count[t]);
+  atomicMax(&k[1], m);
+}
+
+// Row form: one wave per source row, slots assigned in ascending target order
+// by a ballot prefix count.
+__global__ void ell_rows_kernel(const double* __restrict__ dense, int S, int A, int K,
+                                int32_t* __restrict__ row_idx, double* __restrict__ row_val) {
+  const int lane = threadIdx.x & (kWave - 1);
+  const int s = blockIdx.x * (blockDim.x / kWave) + threadIdx.x / kWave;
+  if (s >= S) return;
+  int base = 0;
+  for (int t0 = 0; t0 < S; t0 += kWave) {
+    const int t = t0 + lane;
+    const bool nz = t < S && ell_nz(dense, (size_t)S, A, (size_t)s, (size_t)t);
+    const unsigned long long mask = __ballot(nz);
+    if (nz) {
+      const int slot = base + __popcll(mask & ((1ull << lane) - 1ull));
+      row_idx[(size_t)slot * S + s] = t;
+      for (int a = 0; a < A; ++a) row_val[((size_t)a * K + slot) * S + s] = dense[((size_t)s * S + t) * A + a];
+    }
+    base += __popcll(mask);
+  }
+  for (int slot = base + lane; slot < K; slot += kWave) {  // padding: self, value 0
+    row_idx[(size_t)slot * S + s] = s;
+    for (int a = 0; a < A; ++a) row_val[((size_t)a * K + slot) * S + s] = 0.0;
+  }
+}
+
+// Column form: one thread per target column, scanning sources in ascending
+// order (neighbouring lanes read neighbouring columns: coalesced).
+__global__ void ell_cols_kernel(const double* __restrict__ dense, int S, int A, int K,
+                                int32_t* __restrict__ col_idx, double* __restrict__ col_val) {
+  const int t = blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= S) return;
+  int slot = 0;
+  for (int s = 0; s < S; ++s) {
+    if (!ell_nz(dense, (size_t)S, A, (size_t)s, (size_t)t)) continue;
+    col_idx[(size_t)slot * S + t] = s;
+    for (int a = 0; a < A; ++a) col_val[((size_t)a * K + slot) * S + t] = dense[((size_t)s * S + t) * A + a];
+    ++slot;
+  }
+  for (; slot < K; ++slot) {
+    col_idx[(size_t)slot * S + t] = t;
+    for (int a = 0; a < A; ++a) col_val[((size_t)a * K + slot) * S + t] = 0.0;
+  }
+}
+
+}  // namespace irlmx
+
+extern "C" int irlmx_dense_ell_sizes(const double* dense, int32_t n_states, int32_t n_actions, int32_t* k_out,
+                                     int32_t* col_count, void* stream) {
+  if (n_states <= 0 || n_actions <= 0 || !dense || !k_out || !col_count) {
+    set_error("dense_ell_sizes: bad arguments");
+    return IRLMX_EINVAL;
+  }
+  hipStream_t st = (hipStream_t)stream;
+  hipError_t e = hipMemsetAsync(k_out, 0, 2 * sizeof(int32_t), st);
+  if (e == hipSuccess) e = hipMemsetAsync(col_count, 0, sizeof(int32_t) * (size_t)n_states, st);
+  if (e != hipSuccess) return hip_fail(e, "memset");
+  const int rows_per_block = 256 / kWave;
+  hipLaunchKernelGGL(ell_count_kernel, dim3((n_states + rows_per_block - 1) / rows_per_block), dim3(256), 0, st,
+                     dense, n_states, n_actions, k_out, col_count);
+  hipLaunchKernelGGL(ell_colmax_kernel, dim3(std::min(256, (n_states + 255) / 256)), dim3(256), 0, st, col_count,
+                     n_states, k_out);
+  e = hipGetLastError();
+  return e == hipSuccess ? 0 : hip_fail(e, "ell_count_kernel");
+}
+
+extern "C" int irlmx_dense_to_ell(const double* dense, int32_t n_states, int32_t n_actions, int32_t k_row,
+                                  int32_t k_col, int32_t* row_idx, double* row_val, int32_t* col_idx,
+                                  double* col_val, void* stream) {
+  if (n_states <= 0 || n_actions <= 0 || k_row <= 0 || k_col <= 0 || !dense || !row_idx || !row_val ||
+      !col_idx || !col_val) {
+    set_error("dense_to_ell: bad arguments");
+    return IRLMX_EINVAL;
+  }
+  hipStream_t st = (hipStream_t)stream;
+  const int rows_per_block = 256 / kWave;
+  hipLaunchKernelGGL(ell_rows_kernel, dim3((n_states + rows_per_block - 1) / rows_per_block), dim3(256), 0, st,
+                     dense, n_states, n_actions, k_row, row_idx, row_val);
+  hipLaunchKernelGGL(ell_cols_kernel, dim3((n_states + 255) / 256), dim3(256), 0, st, dense, n_states, n_actions,
+                     k_col, col_idx, col_val);
+  hipError_t e = hipGetLastError();
+  return e == hipSuccess ? 0 : hip_fail(e, "dense_to_ell kernels");
+}

@@ -71,6 +71,8 @@ SIGNATURES = {
     "irlmx_build_icy_gridworld": (ctypes.c_int, [_I32, _P, _I32, _P, _P]),
     "irlmx_build_gridworld": (ctypes.c_int, [_I32, _I32, _P, _P]),
     "irlmx_dense_to_stencil": (ctypes.c_int, [_P, _I32, _I32, _I32, _P, _P, _P]),
+    "irlmx_dense_ell_sizes": (ctypes.c_int, [_P, _I32, _I32, _P, _P, _P]),
+    "irlmx_dense_to_ell": (ctypes.c_int, [_P, _I32, _I32, _I32, _I32, _P, _P, _P, _P, _P]),
 }
 
 _lib = None

@@ -96,43 +96,34 @@ class DeviceMDP:
             w, h = grid
         else:
             w = h = _is_square(S)
+        dense = torch.from_numpy(p).to(device)
         if w and w * h == S:
-            dense = torch.from_numpy(p).to(device)
             row_val = torch.empty((1, A, 5, S), dtype=torch.float64, device=device)
             flag = torch.zeros(1, dtype=torch.int32, device=device)
             _lib.check(lib.irlmx_dense_to_stencil(_lib.ptr(dense), w, h, A, _lib.ptr(row_val), _lib.ptr(flag),
                                                   _lib.stream_ptr(device)), "dense_to_stencil")
-            off = int(flag.item())
-            del dense
-            if not off:
+            if not int(flag.item()):
                 return cls(_lib.LAYOUT_STENCIL5, S, A, 1, True, row_val, width=w, height=h, device=device)
-        return cls._ell_from_dense(p, device)
+        return cls._ell_from_dense(dense, S, A, device)
 
     @classmethod
-    def _ell_from_dense(cls, p, device):
-        S, _, A = p.shape
-        nz = p != 0.0
-        any_a = nz.any(axis=2)                      # [s, t]
-        # row form: union of targets per source state, ascending
-        k_row = max(1, int(any_a.sum(axis=1).max()))
-        row_idx = np.tile(np.arange(S, dtype=np.int32), (k_row, 1))  # pad: self, value 0
-        row_val = np.zeros((A, k_row, S))
-        src, tgt = np.nonzero(any_a)
-        slot = _slots(src, S)
-        row_idx[slot, src] = tgt
-        row_val[:, slot, src] = p[src, tgt, :].T
-        # column form: union of sources per target state, ascending
-        tgt2, src2 = np.nonzero(any_a.T)
-        k_col = max(1, int(any_a.sum(axis=0).max()))
-        col_idx = np.tile(np.arange(S, dtype=np.int32), (k_col, 1))
-        col_val = np.zeros((A, k_col, S))
-        slot2 = _slots(tgt2, S)
-        col_idx[slot2, tgt2] = src2
-        col_val[:, slot2, tgt2] = p[src2, tgt2, :].T
-        t = lambda a, dt: torch.from_numpy(np.ascontiguousarray(a)).to(device=device, dtype=dt)[None]
-        return cls(_lib.LAYOUT_ELL, S, A, 1, True, t(row_val, torch.float64), row_idx=t(row_idx, torch.int32),
-                   col_idx=t(col_idx, torch.int32), col_val=t(col_val, torch.float64), k_row=k_row,
-                   k_col=k_col, device=device)
+    def _ell_from_dense(cls, dense, S, A, device):
+        """ELL row / column forms of a dense device table (irlmx_dense_to_ell)."""
+        lib = _lib.load()
+        st = _lib.stream_ptr(device)
+        k = torch.empty(2, dtype=torch.int32, device=device)
+        scratch = torch.empty(S, dtype=torch.int32, device=device)
+        _lib.check(lib.irlmx_dense_ell_sizes(_lib.ptr(dense), S, A, _lib.ptr(k), _lib.ptr(scratch), st),
+                   "dense_ell_sizes")
+        k_row, k_col = (max(1, int(v)) for v in k.tolist())
+        row_idx = torch.empty((1, k_row, S), dtype=torch.int32, device=device)
+        row_val = torch.empty((1, A, k_row, S), dtype=torch.float64, device=device)
+        col_idx = torch.empty((1, k_col, S), dtype=torch.int32, device=device)
+        col_val = torch.empty((1, A, k_col, S), dtype=torch.float64, device=device)
+        _lib.check(lib.irlmx_dense_to_ell(_lib.ptr(dense), S, A, k_row, k_col, _lib.ptr(row_idx), _lib.ptr(row_val),
+                                          _lib.ptr(col_idx), _lib.ptr(col_val), st), "dense_to_ell")
+        return cls(_lib.LAYOUT_ELL, S, A, 1, True, row_val, row_idx=row_idx, col_idx=col_idx, col_val=col_val,
+                   k_row=k_row, k_col=k_col, device=device)
 
     # -- views -------------------------------------------------------------
 
@@ -195,9 +186,3 @@ class DeviceMDP:
         return out
 
 
-def _slots(keys, n):
-    """Position of each entry among the entries with the same key (keys sorted)."""
-    if len(keys) == 0:
-        return np.zeros(0, dtype=np.int64)
-    starts = np.searchsorted(keys, np.arange(n))
-    return np.arange(len(keys)) - starts[keys]

@@ -544,3 +544,39 @@ def test_width256_quads_bit_identical(dev, monkeypatch):
         assert torch.equal(out["sweep"][0], out[name][0]), (name, "pi")
         assert torch.equal(out["sweep"][1], out[name][1]), (name, "svf")
         assert torch.equal(out["sweep"][2], out[name][2]), (name, "sweeps")
+
+
+def test_dense_to_ell_device(dev):
+    """irlmx_dense_to_ell: row form = per source the union over actions of its
+    targets, ascending; column form = per target its sources, ascending; unused
+    slots point at the state itself with value 0 -- checked entry by entry
+    against a numpy construction, on random sparse tables with empty rows and
+    columns and a fully dense row."""
+    from irlmx import DeviceMDP
+    rng = np.random.default_rng(11)
+    for S, A in ((37, 3), (300, 4), (130, 1)):
+        P = np.zeros((S, S, A))
+        for s in range(S):
+            if s % 17 == 3:
+                continue                                   # empty row
+            tg = rng.choice(S, size=rng.integers(1, 6), replace=False)
+            for a in range(A):
+                P[s, tg, a] = rng.uniform(0.0, 1.0, tg.size) * (rng.uniform() < 0.8)
+        P[5, :, 0] = 1.0 / S                               # a dense row
+        mdp = DeviceMDP.from_dense(P, device=dev)
+        nz = (P != 0.0).any(axis=2)
+        k_row, k_col = max(1, int(nz.sum(axis=1).max())), max(1, int(nz.sum(axis=0).max()))
+        assert (mdp.k_row, mdp.k_col) == (k_row, k_col)
+        ri, rv = mdp.row_idx[0].cpu().numpy(), mdp.row_val[0].cpu().numpy()
+        ci, cv = mdp.col_idx[0].cpu().numpy(), mdp.col_val[0].cpu().numpy()
+        for s in range(S):
+            tg = np.flatnonzero(nz[s])
+            exp_i = np.concatenate([tg, np.full(k_row - tg.size, s)])
+            assert np.array_equal(ri[:, s], exp_i), (S, s)
+            exp_v = np.concatenate([P[s, tg, :].T, np.zeros((A, k_row - tg.size))], axis=1)
+            assert np.array_equal(rv[:, :, s], exp_v), (S, s)
+            src = np.flatnonzero(nz[:, s])
+            assert np.array_equal(ci[:, s], np.concatenate([src, np.full(k_col - src.size, s)])), (S, s)
+            exp_c = np.concatenate([P[src, s, :].T, np.zeros((A, k_col - src.size))], axis=1)
+            assert np.array_equal(cv[:, :, s], exp_c), (S, s)
+        assert np.array_equal(mdp.to_dense(), P)
