@@ -29,7 +29,7 @@ for v in sys.argv[1:] or [""]:
         k, val = kv.split("=")
         os.environ[k] = val
     if mode == "fwd":
-        call = lambda: ops.forward_svf(mdp, p0, tm, pi)[0:2]
+        call = lambda: ops.forward_svf(mdp, p0, tm, pi, max_iter=int(os.environ.get("MAXITER", "0")))[0:2]
     else:
         call = lambda: (ops.backward_maxent(mdp, r, tm), torch.zeros(1))
     out = call(); torch.cuda.synchronize()
