@@ -18,7 +18,7 @@ tm = ops.terminal_mask([n - 1], n, batch=B, device=dev)
 r = torch.ones((B, n), dtype=torch.float64, device=dev)
 variants = sys.argv[1:] or [""]
 RESC = os.environ.get("RESCALE", "1") != "0"
-keys = ("IRLMX_NT", "IRLMX_PAIR", "IRLMX_CLUSTER_R", "IRLMX_CLUSTER_G", "IRLMX_STAMPS")
+keys = ("IRLMX_NT", "IRLMX_PAIR", "IRLMX_CLUSTER_R", "IRLMX_CLUSTER_G", "IRLMX_STAMPS", "IRLMX_BALANCED")
 ref = None
 for v in variants:
     for k in keys:
