@@ -23,12 +23,14 @@
 // stores then stay in that XCD's L2, where the sc1 loads are served).
 //
 // Convergence (forward).  Per sweep i of a block a tile records "some owned
-// |delta| > eps" (bit i) and "some |delta| is NaN" (bit 16 + i); the OR over
-// tiles arrives with the exchange, so every tile takes the same decision: if
-// the first sweep with !(delta > eps) lies inside the block, every tile reloads
-// the block-start state (an LDS snapshot) and re-runs exactly that many sweeps
-// -- the same arithmetic in the same order, so the result is the one the
-// reference's loop stops at.
+// |delta| > eps" (bit i; a running fmax per lane) and, once per block, "some
+// owned value is non-finite" (bit 31); the OR over tiles arrives with the
+// exchange, so every tile takes the same decision: if the first sweep with
+// !(delta > eps) lies inside the block, every tile reloads the block-start
+// state (an LDS snapshot) and re-runs exactly that many sweeps -- the same
+// arithmetic in the same order, so the result is the one the reference's loop
+// stops at.  Bit 31 hands the call back to the host (exact NaN bookkeeping on
+// the per-sweep shape, see the kernel).
 //
 // Rescaling (backward).  The partition vector grows geometrically.  A first
 // pass bounds the per-sweep growth g of each instance; blocks are capped at
@@ -59,11 +61,10 @@ int hip_fail(hipError_t e, const char* what);
 // feed is a ghost row that is no longer exact).
 //
 // Per-sweep convergence bookkeeping (forward): the reference stops after the
-// first sweep whose max|d_new - d_old| is not > eps, NaN included.  So per
-// sweep i of a block two facts suffice: "some |delta| > eps" (bit i) and "some
-// |delta| is NaN" (bit 16 + i).  Threads collect them in a register, and the
-// tile ORs them once per block (ballots, one LDS atomic per wave, one global
-// atomic per tile) -- no per-sweep reduction.
+// first sweep whose max|d_new - d_old| is not > eps, NaN included.  Threads
+// collect "some |delta| > eps" per sweep (bit i) in a register, and the tile
+// ORs the bits once per block (DPP wave reduction, one LDS atomic per wave) --
+// no per-sweep reduction.  NaN: see the kernel's bookkeeping comment.
 //
 // PAIR (widths 64 and 128): thread slot jp holds the horizontally adjacent
 // states 2p, 2p + 1 (p = tid + jp * NT) and keeps their values in registers
