@@ -999,6 +999,17 @@ int cluster_run(int mode, const ClusterPlan& plan, ClusterArgs a, int B, hipStre
                     "wait %.0f  refresh %.0f  same-xcd %.2f  (publish: stores %.0f, summary %.0f)\n", "lds", p.pair == 3 ? "-quads" : (p.pair == 2 ? "-cols" : (p.pair == 1 ? "-pair" : "")), mode, p.R, p.G, p.C, p.spt,
             acc[4], acc[0] / acc[4], acc[1] / acc[4], acc[2] / acc[4], acc[3] / acc[4], acc[5], acc[6] / acc[4],
             (acc[7] - acc[6]) / acc[4]);
+    if (p.C <= 8) {  // per tile position: the interior tiles carry ghost rows on both sides
+      for (int t = 0; t < p.C; ++t) {
+        double ta[5] = {0, 0, 0, 0, 0};
+        int n = 0;
+        for (int g = t; g < nwg; g += p.C, ++n)
+          for (int k = 0; k < 5; ++k) ta[k] += (double)h[(size_t)g * 8 + k];
+        if (n && ta[4] > 0)
+          fprintf(stderr, "[irlmx stamps]   tile %d: sweeps %.0f  publish %.0f  wait %.0f  refresh %.0f\n", t,
+                  ta[0] / ta[4], ta[1] / ta[4], ta[2] / ta[4], ta[3] / ta[4]);
+      }
+    }
     free(h);
     (void)hipFree(stamps);
   }
