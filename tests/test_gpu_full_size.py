@@ -111,3 +111,20 @@ def test_cluster_forward_nonfinite_rerun(dev, bad, monkeypatch):
     svf_s, k_s, st_s = ops.forward_svf(mdp, p0, tm, pi)
     assert torch.equal(svf_s.view(torch.int64), svf.view(torch.int64))  # bit patterns (NaN included)
     assert torch.equal(k_s, k) and torch.equal(st_s, st)
+
+
+@pytest.mark.parametrize("average", [False, True])
+def test_value_iteration_128_vs_sparse_oracle(dev, average):
+    """solver.value_iteration / stochastic_value_iteration (solver.py:9-104) at
+    128x128 on the device (per-sweep shape) against the sparse-operand oracle:
+    identical sweep count, values within 1e-9."""
+    from irlmx import DeviceMDP, ops
+    size = 128
+    n = size * size
+    r = np.random.default_rng(17).uniform(0.0, 1.0, n)
+    mdp = DeviceMDP.icy_gridworld(size, 0.2, device=dev)
+    v, k, st = ops.value_iteration(mdp, r, 0.9, average=average)
+    v_ref, k_ref = O.value_iteration_csr(O.icy_gridworld_csr(size, 0.2), r, 0.9, average=average)
+    assert int(k[0]) == k_ref and int(st[0]) == 0
+    e = rel_err(v[0].cpu().numpy(), v_ref)
+    assert e <= CONTRACT and e <= RTOL, e

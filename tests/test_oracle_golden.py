@@ -172,3 +172,16 @@ def test_sparse_oracle_matches_dense():
         d, k = O.forward_svf(P, p0, [n - 1], pi)
         d_s, k_s = O.forward_svf_csr(mats, p0, [n - 1], pi)
         assert k == k_s and np.max(np.abs(d_s - d)) <= 1e-12 * np.max(d)
+
+
+def test_sparse_value_iteration_matches_dense():
+    rng = np.random.default_rng(9)
+    for size in (5, 16):
+        n = size * size
+        P = O.icy_gridworld_table(size, 0.2)
+        mats = O.icy_gridworld_csr(size, 0.2)
+        r = rng.uniform(0.0, 1.0, n)
+        for avg in (False, True):
+            v, k = O.value_iteration(P, r, 0.9, average=avg)
+            vs, ks = O.value_iteration_csr(mats, r, 0.9, average=avg)
+            assert k == ks and np.max(np.abs(vs - v)) <= 1e-12 * np.max(np.abs(v))
