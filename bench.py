@@ -153,12 +153,18 @@ def cpu_baseline(size, p_slip, k_b, k_f, n_sweeps):
     }
 
 
+def rank_env():
+    return int(os.environ.get("RANK", "0"))
+
+
 def main():
     args = parse()
     import torch
     import torch.distributed as dist
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
+    if args.gpus != world and rank_env() == 0:
+        print(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world}; reporting {world} GPU(s)", file=sys.stderr)
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world > 1:
