@@ -35,11 +35,14 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, os.path.join(ROOT, "irl-maxent_amd"))
 
 CONFIGS = {
-    # name: (grid size, instances per GPU, description)
-    "c3": (128, 64, "BASELINE config 3: 128x128 IcyGridWorld, batch 64 per GPU, fp64"),
-    "c2": (64, 1, "BASELINE config 2 (A=4 pinned variant): 64x64 IcyGridWorld, 1 instance"),
-    "c4": (256, 32, "BASELINE config 4: 256x256 IcyGridWorld, 32 instances per GPU"),
+    # name: (grid size, instances per GPU, description, causal)
+    "c3": (128, 64, "BASELINE config 3: 128x128 IcyGridWorld, batch 64 per GPU, fp64", False),
+    "c2": (64, 1, "BASELINE config 2 (A=4 pinned variant): 64x64 IcyGridWorld, 1 instance", False),
+    "c4": (256, 32, "BASELINE config 4: 256x256 IcyGridWorld, 32 instances per GPU", False),
+    "c5": (128, 1, "BASELINE config 5: MaxCausalEnt (soft VI, discount 0.7) on 128x128 IcyGridWorld, "
+                   "1 instance per GPU, fp64", True),
 }
+DISCOUNT = 0.7   # src/main.py's irl_causal discount
 
 HBM_PEAK_GBS = 8000.0          # MI355X_MICROARCH.md: 8.0 TB/s spec
 BYTES_FWD = 168                # forward sweep, bytes per state per instance
@@ -48,6 +51,7 @@ BYTES_BWD = 152                # backward sweep
 # point of the collapsed 5-point stencil = 10 flop; the forward adds p0 (+1)
 FLOP_BWD = 10
 FLOP_FWD = 11
+FLOP_SOFT = 4 * 11             # soft VI: per action 5 FMA + the discount scale (exp/log not counted)
 FP64_PEAK_TFS = 78.6           # MI355X FP64 vector (= FP64 matrix) spec peak
 FP64_LOOP_TFS = 54.8           # tools/diag/dfma_rate.hip mode 0: independent fp64 FMA chains, 2 waves/SIMD
 
@@ -77,19 +81,19 @@ def _latest_traffic():
 CPU_DENSE_MAX = 128   # larger dense fp64 tables do not fit host RAM (256x256: 137 GB); extrapolate
 
 
-def cpu_baseline(size, p_slip, k_b, k_f, n_sweeps):
+def cpu_baseline(size, p_slip, k_b, k_f, n_sweeps, causal=False):
     """Time the reference's dense statements on one instance (oracle restatement).
 
     Above 128x128 the dense table does not fit in host memory: the statements are
     timed at 128x128 and scaled by the dense work ratio (S / 16384)^2, labelled
     "extrapolated" (SURVEY.md 8(d))."""
     if size > CPU_DENSE_MAX:
-        base = cpu_baseline(CPU_DENSE_MAX, p_slip, k_b, k_f, n_sweeps)
+        base = cpu_baseline(CPU_DENSE_MAX, p_slip, k_b, k_f, n_sweeps, causal)
         ratio = (size * size / float(CPU_DENSE_MAX * CPU_DENSE_MAX)) ** 2
         base["value"] /= ratio
         base["sample"] = (f"extrapolated: {size}x{size} dense fp64 does not fit host RAM; per-sweep and copy "
                           f"times measured at {CPU_DENSE_MAX}x{CPU_DENSE_MAX} x (S ratio)^2 = {ratio:.0f}, with "
-                          f"this run's K_b={k_b}, K_f={k_f:.0f} -- " + base["sample"])
+                          f"this run's K_b={k_b:.0f}, K_f={k_f:.0f} -- " + base["sample"])
         return base
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import maxent_oracle as O
@@ -129,6 +133,22 @@ def cpu_baseline(size, p_slip, k_b, k_f, n_sweeps):
         za = np.array([er * bw[a].dot(zs) for a in range(4)]).T
         return za.sum(axis=1)
 
+    phi = O.terminal_reward(terminal, S)
+    r = np.ones(S)
+
+    def soft_sweep(v):  # maxent.py:329-338
+        q = np.array([r + DISCOUNT * bw[a].dot(v) for a in range(4)]).T
+        nv = phi
+        for a in range(4):
+            nv = O.softmax2(nv, q[:, a])
+        nv = np.array(nv, dtype=float)
+        np.max(np.abs(nv - v))
+        return nv
+
+    if causal:
+        bwd_sweep = soft_sweep   # noqa: F811 (same timing loop below)
+        zs = -1e200 * np.ones(S)
+
     for _ in range(2):
         fwd_sweep(d)
         bwd_sweep(zs)
@@ -138,7 +158,7 @@ def cpu_baseline(size, p_slip, k_b, k_f, n_sweeps):
     t_f = (time.perf_counter() - t0) / n_sweeps
     t0 = time.perf_counter()
     for _ in range(n_sweeps):
-        zs = bwd_sweep(zs) * 1e-3
+        zs = bwd_sweep(zs) if causal else bwd_sweep(zs) * 1e-3
     t_b = (time.perf_counter() - t0) / n_sweeps
     t_step = k_b * t_b + k_f * t_f + t_copy
     return {
@@ -147,9 +167,10 @@ def cpu_baseline(size, p_slip, k_b, k_f, n_sweeps):
         "cores": int(threads),
         "kind": "port",
         "sample": (f"dense fp64 {size}x{size} (S={S}, A=4), one instance: {n_sweeps} timed sweeps each of "
-                   f"maxent.py:109-112 (forward, {t_f * 1e3:.1f} ms) and :155-156 (backward, {t_b * 1e3:.1f} ms) "
-                   f"+ one call's copies maxent.py:98-102,143 ({t_copy:.2f} s); step = K_b*t_b + K_f*t_f + t_copy "
-                   f"with this run's K_b={k_b}, K_f={k_f:.0f}; table build {t_build:.1f} s untimed"),
+                   f"maxent.py:109-112 (forward, {t_f * 1e3:.1f} ms) and "
+                   f"{':329-338 (soft VI' if causal else ':155-156 (backward'}, {t_b * 1e3:.1f} ms) "
+                   f"+ one call's copies maxent.py:98-102,{320 if causal else 143} ({t_copy:.2f} s); step = K_b*t_b + K_f*t_f + t_copy "
+                   f"with this run's K_b={k_b:.0f}, K_f={k_f:.0f}; table build {t_build:.1f} s untimed"),
     }
 
 
@@ -177,7 +198,7 @@ def main():
     from irlmx import DeviceMDP, demos
     from irlmx.batch import BatchedMaxEnt
 
-    size, per_gpu, desc = CONFIGS[args.config]
+    size, per_gpu, desc, causal = CONFIGS[args.config]
     size = args.size or size
     per_gpu = args.batch or per_gpu
     S = size * size
@@ -194,7 +215,7 @@ def main():
     p_0 = np.empty((per_gpu, S))
     for i, b in enumerate(ids):
         e_f[i], p_0[i], _ = demos.sample(rv[i], size, terminal, 0, n=200, seed=1234 + int(b))
-    irl = BatchedMaxEnt(mdp, e_f, p_0, terminal)
+    irl = BatchedMaxEnt(mdp, e_f, p_0, terminal, causal=causal, discount=DISCOUNT if causal else None)
     torch.cuda.synchronize()
 
     def barrier():
@@ -210,7 +231,7 @@ def main():
     stream = torch.cuda.current_stream(dev)
     ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True),
            torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
-    sweeps = []
+    sweeps, bsweeps = [], []
     t0 = time.perf_counter()
     for i in range(args.steps):
         e0, e1, e2 = ev[i]
@@ -221,6 +242,8 @@ def main():
         e2.record(stream)
         irl.update(svf)
         sweeps.append(iters)
+        if causal:
+            bsweeps.append(irl.last_backward_sweeps)
     torch.cuda.synchronize()
     barrier()
     torch.cuda.synchronize()
@@ -229,13 +252,16 @@ def main():
     elapsed_max = max_over_ranks(elapsed, dev)
 
     k_f = torch.stack(sweeps).to(torch.float64)           # [steps, B]
+    # backward sweeps per instance and step: 2S-1 collapsed + 1 (maxent.py:151-156), or soft VI's count
+    k_b = torch.stack(bsweeps).to(torch.float64) if causal else torch.full_like(k_f, float(2 * S))
     t_bwd = sum(e0.elapsed_time(e1) for e0, e1, _ in ev) * 1e-3
     t_fwd = sum(e1.elapsed_time(e2) for _, e1, e2 in ev) * 1e-3
     # SURVEY 8(d) algorithmic bytes: per instance and sweep 152*S (backward), 168*S (forward)
-    bwd_bytes = BYTES_BWD * S * float(2 * S) * per_gpu * args.steps
+    bwd_bytes = BYTES_BWD * S * float(k_b.sum())
     fwd_bytes = BYTES_FWD * S * float(k_f.sum())
     kern = {"backward": {"bytes": bwd_bytes, "seconds": t_bwd, "launches": args.steps,
-                         "flop": FLOP_BWD * S * float(2 * S - 1) * per_gpu * args.steps},
+                         "flop": (FLOP_SOFT * S * float(k_b.sum()) if causal
+                                  else FLOP_BWD * S * float(2 * S - 1) * per_gpu * args.steps)},
             "forward": {"bytes": fwd_bytes, "seconds": t_fwd, "launches": args.steps,
                         "flop": FLOP_FWD * S * float(k_f.sum())}}
     dom = max(kern, key=lambda k: kern[k]["seconds"])
@@ -257,7 +283,7 @@ def main():
             "config": {"workload": desc, "grid": f"{size}x{size}", "n_states": S, "n_actions": 4,
                        "batch_per_gpu": per_gpu, "global_batch": B_total, "eps_svf": 1e-5,
                        "parallelism": f"instances sharded over {world} GPU(s), no collective"},
-            "sweeps": {"backward_per_step": 2 * S, "forward_mean": float(k_f.mean()),
+            "sweeps": {"backward_per_step": float(k_b.mean()), "forward_mean": float(k_f.mean()),
                        "forward_max": float(k_f.max())},
             "phase_s": {"backward": t_bwd, "forward": t_fwd},
             "roofline": {"bound": "hbm", "kernel": f"{dom} pass (one launch per step covers every instance "
@@ -292,8 +318,8 @@ def main():
                 out["roofline"]["traffic_source"] = (f"{os.path.relpath(tpath, ROOT)}: FETCH_SIZE + WRITE_SIZE "
                                                      f"(KiB x 1024) of one {dom} dispatch, separate --pmc passes")
         if world == 1 and not args.no_cpu_baseline:
-            out["cpu_baseline"] = cpu_baseline(size, float(slips[0]), 2 * S, float(k_f[:, 0].mean()),
-                                               args.cpu_sweeps)
+            out["cpu_baseline"] = cpu_baseline(size, float(slips[0]), float(k_b[:, 0].mean()),
+                                               float(k_f[:, 0].mean()), args.cpu_sweeps, causal)
             out["speedup_vs_cpu"] = out["value"] / out["cpu_baseline"]["value"]
         print(json.dumps(out), flush=True)
     if world > 1:

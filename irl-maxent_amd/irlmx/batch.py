@@ -76,6 +76,7 @@ class BatchedMaxEnt:
         self.active = torch.ones(B, dtype=torch.bool, device=dev)
         self.steps = torch.zeros(B, dtype=torch.int64, device=dev)
         self.last_forward_sweeps = None
+        self.last_backward_sweeps = None   # causal: soft VI sweeps of the last backward() [B]
         self.last_delta = None
 
     def lr(self, k):
@@ -100,7 +101,8 @@ class BatchedMaxEnt:
     def backward(self):
         r = self.reward()
         if self.causal:
-            pi, _, _, _ = ops.soft_backward(self.mdp, r, self.phi, self.discount, self.eps_lap)
+            pi, _, k, _ = ops.soft_backward(self.mdp, r, self.phi, self.discount, self.eps_lap)
+            self.last_backward_sweeps = k
             return pi
         return ops.backward_maxent(self.mdp, r, self.terminal, rescale=self.rescale)
 
