@@ -165,6 +165,7 @@ def cpu_baseline(size, p_slip, k_b, k_f, n_sweeps, causal=False):
         "value": 1.0 / t_step,
         "unit": "instance-steps/s",
         "cores": int(threads),
+        "host_cpu_count": os.cpu_count(),
         "kind": "port",
         "sample": (f"dense fp64 {size}x{size} (S={S}, A=4), one instance: {n_sweeps} timed sweeps each of "
                    f"maxent.py:109-112 (forward, {t_f * 1e3:.1f} ms) and "
@@ -172,6 +173,25 @@ def cpu_baseline(size, p_slip, k_b, k_f, n_sweeps, causal=False):
                    f"+ one call's copies maxent.py:98-102,{320 if causal else 143} ({t_copy:.2f} s); step = K_b*t_b + K_f*t_f + t_copy "
                    f"with this run's K_b={k_b:.0f}, K_f={k_f:.0f}; table build {t_build:.1f} s untimed"),
     }
+
+
+def stream_copy_gbs(dev, nbytes=1 << 30, reps=5):
+    """Device-to-device copy rate (read + write bytes / time) on this GPU: the
+    achievable-HBM reference SURVEY.md 8(d) asks for beside the 8 TB/s spec."""
+    import torch
+    a = torch.empty(nbytes // 8, dtype=torch.float64, device=dev).fill_(1.0)
+    c = torch.empty_like(a)
+    c.copy_(a)
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(reps):
+        c.copy_(a)
+    e1.record()
+    torch.cuda.synchronize()
+    gbs = 2.0 * nbytes * reps / (e0.elapsed_time(e1) * 1e-3) / 1e9
+    del a, c
+    torch.cuda.empty_cache()
+    return gbs
 
 
 def rank_env():
@@ -310,6 +330,7 @@ def main():
                                v["launches"] * 1e3, "achieved_TFLOPs": v["flop"] / v["seconds"] / 1e12}
                            for k, v in kern.items()},
         }
+        out["roofline"]["stream_copy_GBs"] = stream_copy_gbs(dev)
         tpath = args.traffic or _latest_traffic()
         if tpath and os.path.exists(tpath) and args.config == "c3" and not args.size and not args.batch:
             tr = json.load(open(tpath)).get(dom)
