@@ -876,7 +876,12 @@ bool cluster_plan(int W, int H, int B, int mode, ClusterPlan* out) {
       // (a single tile per instance needs no hand-off: ~0.8k cycles of block
       // bookkeeping; a sweep takes at least ~850 cycles of barrier, LDS and
       // FMA-chain latency however few states a lane holds)
-      const double xchg = (C == 1 && W == 64 && layout > 0) ? 800.0 : xcd_groupable(std::min(per, B), C) ? 5000.0 : 11000.0;
+      const bool solo = C == 1 && W == 64 && layout > 0;
+      double xchg = solo ? 800.0 : xcd_groupable(std::min(per, B), C) ? 5000.0 : 11000.0;
+      // the forward's block end waits for the convergence words of all C tiles
+      // of an instance: ~120 cycles more per tile (measured at one 128x128 /
+      // 64x64 instance, C = 8..32: tools/diag/plan_bench.py)
+      if (mode == kModeFwd && !solo) xchg += 120.0 * (C - 16);
       // (the forward's convergence bookkeeping: ~165 cycles per slot)
       const double cost = nl * (std::max((mode == kModeFwd ? 165.0 : 110.0) * spt, 850.0) * G + xchg) / G;
       if (cost < best - 1e-9) {
