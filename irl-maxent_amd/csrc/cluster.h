@@ -63,6 +63,9 @@ struct ClusterPlan {
 // counter, no fence, one fabric round trip per exchange.  Tag = per-launch
 // salt | (block + 1); the workspace is also zeroed before every call.
 typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+#ifndef IRLMX_POLL_SLEEP
+#define IRLMX_POLL_SLEEP 1   // s_sleep units (64 cycles) between polling passes
+#endif
 constexpr int kGatherPerThread = 4;
 
 __device__ inline __amdgpu_buffer_rsrc_t gran_rsrc(const void* base, unsigned bytes) {
@@ -98,7 +101,7 @@ __device__ inline bool gran_gather(__amdgpu_buffer_rsrc_t r, __amdgpu_buffer_rsr
       }
     if (!pending) break;
     if (__builtin_amdgcn_s_memrealtime() - t0 > 2000000000ull) return false;
-    __builtin_amdgcn_s_sleep(1);
+    __builtin_amdgcn_s_sleep(IRLMX_POLL_SLEEP);
   }
   return true;
 }

@@ -514,6 +514,41 @@ def test_cluster_multi_launch_and_edge_cases(dev, monkeypatch):
     assert len(set(b[2].tolist())) > 2                                # instances stop at different sweeps
 
 
+def test_cluster_stops_at_block_edges(dev, monkeypatch):
+    """Cluster forward stopping inside the first block, on the last sweep of a
+    block, one sweep into the next, at an early eps-convergence and at the
+    natural one -- against the per-sweep shape, bit for bit (SVFs, sweep counts,
+    MAXITER / OK status), three instances per launch (T = G = 6 sweeps per block)."""
+    from irlmx import DeviceMDP, ops
+    size, B = 64, 3
+    n = size * size
+    mdp = DeviceMDP.icy_gridworld(size, [0.1, 0.2, 0.3], device=dev)
+    r = np.ones((B, n))   # (random rewards mix far more slowly: millions of sweeps)
+    tm = ops.terminal_mask([n - 1], n, batch=B, device=dev)
+    p0 = np.zeros((B, n))
+    p0[np.arange(B), [0, 100, 2000]] = 1.0
+    keys = ("IRLMX_FUSED_MAX_STATES", "IRLMX_CLUSTER", "IRLMX_CLUSTER_R", "IRLMX_CLUSTER_G")
+    for k in keys:
+        monkeypatch.delenv(k, raising=False)
+    pi = ops.backward_maxent(mdp, r, tm)
+    shapes = (("sweep", {"IRLMX_FUSED_MAX_STATES": "0", "IRLMX_CLUSTER": "0"}),
+              ("cluster", {"IRLMX_CLUSTER_R": "8", "IRLMX_CLUSTER_G": "6"}))
+    for eps, cap in ((1e-5, 1), (1e-5, 5), (1e-5, 6), (1e-5, 7), (1e-5, 13), (2e-3, 0), (1e-5, 0)):
+        out = {}
+        for name, env in shapes:
+            for k in keys:
+                monkeypatch.delenv(k, raising=False)
+            for k, v in env.items():
+                monkeypatch.setenv(k, v)
+            out[name] = ops.forward_svf(mdp, p0, tm, pi, eps=eps, max_iter=cap)
+        for i, what in enumerate(("svf", "sweeps", "status")):
+            assert torch.equal(out["sweep"][i], out["cluster"][i]), (eps, cap, what)
+        if cap:
+            assert out["cluster"][1].tolist() == [cap] * B
+    for k in keys:
+        monkeypatch.delenv(k, raising=False)
+
+
 def test_width256_quads_bit_identical(dev, monkeypatch):
     """Width 256 (config 4's grid): column quads (default) == per-state LDS
     layout == per-sweep shape, bit for bit, backward and a capped forward, two

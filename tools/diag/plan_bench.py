@@ -18,7 +18,8 @@ tm = ops.terminal_mask([n - 1], n, batch=B, device=dev)
 rng = np.random.default_rng(5)
 r = torch.as_tensor(rng.uniform(0, 1.5, (B, n)) if os.environ.get("RAND") else np.ones((B, n)), device=dev)
 p0 = torch.zeros((B, n), dtype=torch.float64, device=dev); p0[:, 0] = 1.0
-keys = ("IRLMX_NT", "IRLMX_PAIR", "IRLMX_CLUSTER_R", "IRLMX_CLUSTER_G", "IRLMX_STAMPS", "IRLMX_CLUSTER", "IRLMX_FUSED")
+keys = ("IRLMX_NT", "IRLMX_PAIR", "IRLMX_CLUSTER_R", "IRLMX_CLUSTER_G", "IRLMX_STAMPS", "IRLMX_CLUSTER", "IRLMX_FUSED",
+        "IRLMX_DEFER")
 pi = ops.backward_maxent(mdp, r, tm)
 torch.cuda.synchronize()
 ref = None
