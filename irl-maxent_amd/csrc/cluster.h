@@ -13,6 +13,10 @@ constexpr int kSptMax = 6;         // states per thread, per-state layout (no VG
 constexpr int kPairThreads = 512;  // threads per workgroup, pair layouts (256 VGPRs)
 constexpr int kSptMaxPair = 12;    // states per thread, pair layouts -> extended tile <= 6144 states
 constexpr int kSptMaxQuadFwd = 12;  // forward with column quads (register budget)
+// backward with column quads: 16 states per lane (32 rows at width 256; ~30
+// VGPRs spill to scratch, yet 3.8 % faster at config 4 than 12: G = 8 ghost
+// rows instead of 4 halve the exchanges)
+constexpr int kSptMaxQuadBwd = 16;
 constexpr int kTMax = 16;          // max sweeps per block (= max ghost rows)
 constexpr int kRescaleEvery = 4;   // backward: max blocks between rescales
 constexpr size_t kMaxLdsBytes = 160 * 1024;  // LDS per CU (one workgroup per CU)

@@ -848,7 +848,10 @@ bool cluster_plan(int W, int H, int B, int mode, ClusterPlan* out) {
   const bool pair = layout > 0;
   const int nt = pair ? kPairThreads : kCT;
   // register budget per lane: the forward's convergence bookkeeping needs more
-  const int spt_max = !pair ? kSptMax : (mode == kModeFwd && layout == 3 ? kSptMaxQuadFwd : kSptMaxPair);
+  // (IRLMX_SPT_MAX: experiments only)
+  const int spt_max = env_int("IRLMX_SPT_MAX", !pair ? kSptMax
+                                              : layout == 3 ? (mode == kModeFwd ? kSptMaxQuadFwd : kSptMaxQuadBwd)
+                                                            : kSptMaxPair);
   const int rows_cap = nt * spt_max / W;
   double best = 1e300;
   bool ok = false;
@@ -928,6 +931,7 @@ static void* cluster_fn_quad(int spt) {
     case 4: return (void*)&cluster_kernel<MODE, 4, WT, 3, kPairThreads>;
     case 8: return (void*)&cluster_kernel<MODE, 8, WT, 3, kPairThreads>;
     case 12: return (void*)&cluster_kernel<MODE, 12, WT, 3, kPairThreads>;
+    case 16: return (void*)&cluster_kernel<MODE, 16, WT, 3, kPairThreads>;
   }
   return nullptr;
 }
