@@ -128,3 +128,49 @@ def test_value_iteration_128_vs_sparse_oracle(dev, average):
     assert int(k[0]) == k_ref and int(st[0]) == 0
     e = rel_err(v[0].cpu().numpy(), v_ref)
     assert e <= CONTRACT and e <= RTOL, e
+
+
+def test_config2_stay_variant_vs_sparse_oracle(dev):
+    """BASELINE config 2's A = 5 variant (IcyGridWorld's four
+    moves plus a "stay" action, 64x64, unpinned by the reference's own tests):
+    uploaded as a dense [S, S, 5] table (STENCIL5 layout, the stay action on
+    the self slot) and checked against the sparse-operand oracle -- backward
+    2*S sweeps, a capped and an eps-converged forward (sweep counts equal,
+    SVF within 1e-9 relative), soft VI and hard-max VI."""
+    import scipy.sparse as sp
+    from irlmx import DeviceMDP, _lib, ops
+    from irlmx.batch import terminal_reward
+    size, n = 64, 64 * 64
+    mats = O.icy_gridworld_csr(size, 0.2) + [sp.identity(n, format="csr")]
+    dense = np.zeros((n, n, 5))
+    for a, m in enumerate(mats):
+        c = m.tocoo()
+        dense[c.row, c.col, a] = c.data
+    mdp = DeviceMDP.from_dense(dense, device=dev)
+    del dense
+    assert mdp.layout == _lib.LAYOUT_STENCIL5 and mdp.n_actions == 5
+    rng = np.random.default_rng(12)
+    r = rng.uniform(0.0, 1.0, n)
+    term = [n - 1]
+    tm = ops.terminal_mask(term, n, device=dev)
+    for rb in (r, np.ones(n)):
+        pi = ops.backward_maxent(mdp, rb, tm)[0].cpu().numpy()
+        ref_pi = O.backward_maxent_csr(mats, term, rb)
+        assert np.max(np.abs(pi - ref_pi)) <= 1e-9 * np.max(np.abs(ref_pi))
+    p0 = np.zeros(n)
+    p0[0] = 1.0
+    # (the forward from theta = 1's policy: random rewards mix over millions of sweeps)
+    for eps, cap in ((1e-5, 3000), (2e-3, 0)):
+        svf, k, st = ops.forward_svf(mdp, p0, tm, ref_pi, eps=eps, max_iter=cap)
+        ref_svf, ref_k = O.forward_svf_csr(mats, p0, term, ref_pi, eps=eps, max_iter=cap or None)
+        assert int(k[0]) == ref_k, (eps, cap, int(k[0]), ref_k)
+        assert np.max(np.abs(svf[0].cpu().numpy() - ref_svf)) <= 1e-9 * np.max(np.abs(ref_svf))
+    v, kv, _ = ops.value_iteration(mdp, r, 0.9)
+    ref_v, ref_kv = O.value_iteration_csr(mats, r, 0.9)
+    assert int(kv[0]) == ref_kv
+    assert np.max(np.abs(v[0].cpu().numpy() - ref_v)) <= 1e-12 * np.max(np.abs(ref_v))
+    cpi, cv, ks, _ = ops.soft_backward(mdp, r, terminal_reward(term, n, 1, dev), 0.7)
+    ref_cpi, ref_cv, ref_ks = O.soft_backward_csr(mats, term, r, 0.7)
+    assert int(ks[0]) == ref_ks
+    assert np.max(np.abs(cpi[0].cpu().numpy() - ref_cpi)) <= 1e-9 * np.max(np.abs(ref_cpi))
+    assert np.max(np.abs(cv[0].cpu().numpy() - ref_cv)) <= 1e-9 * np.max(np.abs(ref_cv))

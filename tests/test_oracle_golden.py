@@ -174,6 +174,25 @@ def test_sparse_oracle_matches_dense():
         assert k == k_s and np.max(np.abs(d_s - d)) <= 1e-12 * np.max(d)
 
 
+def test_sparse_soft_backward_matches_dense():
+    """soft_backward_csr (the config-2 stay-variant check in test_gpu_full_size.py)
+    against the dense restatement, which the causal golden vectors pin: the
+    same sweep count, policy and values to rounding -- including a 5-action
+    table (the four moves plus "stay")."""
+    import scipy.sparse as sp
+    rng = np.random.default_rng(10)
+    for size, stay in ((5, False), (12, False), (12, True)):
+        n = size * size
+        mats = O.icy_gridworld_csr(size, 0.2) + ([sp.identity(n, format="csr")] if stay else [])
+        P = np.stack([m.toarray() for m in mats], axis=2)
+        r = rng.uniform(0.0, 1.0, n)
+        pi, v, k = O.soft_backward(P, [n - 1], r, 0.7)
+        pi_s, v_s, k_s = O.soft_backward_csr(mats, [n - 1], r, 0.7)
+        assert k == k_s, (size, stay)
+        assert np.max(np.abs(pi_s - pi)) <= 1e-12 * np.max(pi)
+        assert np.max(np.abs(v_s - v)) <= 1e-12 * np.max(np.abs(v))
+
+
 def test_sparse_value_iteration_matches_dense():
     rng = np.random.default_rng(9)
     for size in (5, 16):
