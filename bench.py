@@ -13,14 +13,23 @@ per GPU (weak scaling), instance b has p_slip = 0.1 + 0.2*b/B_total, terminal
 expert trajectories per instance (irlmx.demos, seed 1234 + b).  Inputs are
 resident in HBM before the timed region.
 
+The headline times K steps after W warm-up steps (steady state: the first
+step's forward pass runs ~360k sweeps, later ones ~650).  ``first_steps``
+reports the run from theta0 = 1 including step 1: steps 1..25 timed one by one
+(the warm-up and timed steps are its first W + K; more are run after the timed
+region when W + K < 25).
+
 Multi-GPU: one process per GPU (torch.distributed.run); instances are sharded
-in contiguous blocks with no collective on the data path; the only collectives
-are the timing barrier and the max-over-ranks of the elapsed time.
+in contiguous blocks with no collective on the data path.  The process group
+is gloo (host-side): it carries only the timing barrier and the max-over-ranks
+of the elapsed time, so RCCL is never initialised.
 
 The CPU baseline (rank 0, N = 1) times the reference's own dense numpy
 statements (oracle/maxent_oracle.py restates them; maxent.py:98-112, 143-156)
 on one instance of the same workload for a bounded sample of sweeps, and
-extrapolates with the sweep counts this run logged.
+extrapolates with the sweep counts this run logged (mean over instances);
+``config1`` times BASELINE config 1 (src/main.py's 5x5 problem: full irl and
+irl_causal runs) on the device drop-in and on the oracle, in the same run.
 """
 
 import argparse
@@ -43,20 +52,23 @@ CONFIGS = {
                    "1 instance per GPU, fp64", True),
 }
 DISCOUNT = 0.7   # src/main.py's irl_causal discount
+FIRST_STEPS = 25
 
 HBM_PEAK_GBS = 8000.0          # MI355X_MICROARCH.md: 8.0 TB/s spec
 BYTES_FWD = 168                # forward sweep, bytes per state per instance
 BYTES_BWD = 152                # backward sweep
-# fp64 arithmetic the sweeps execute per state: one FMA per
-# point of the collapsed 5-point stencil = 10 flop; the forward adds p0 (+1)
+BYTES_SOFT = 224               # soft-VI sweep
+# fp64 arithmetic per state and sweep: the collapsed
+# 5-point stencil is one FMA per point = 10 flop; the forward adds p0 (+1); soft
+# VI per action 5 FMAs and the discount product (exp / log not counted)
 FLOP_BWD = 10
 FLOP_FWD = 11
-FLOP_SOFT = 4 * 11             # soft VI: per action 5 FMA + the discount scale (exp/log not counted)
-FP64_PEAK_TFS = 78.6           # MI355X FP64 vector (= FP64 matrix) spec peak
+FLOP_SOFT = 4 * 11
+FP64_PEAK_TFS = 78.6           # MI355X FP64 vector (= FP64 matrix) spec peak, MI355X_MICROARCH.md
 FP64_LOOP_TFS = 54.8           # tools/diag/dfma_rate.hip mode 0: independent fp64 FMA chains, 2 waves/SIMD
 
 
-def parse():
+def parse(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=3)
@@ -65,49 +77,53 @@ def parse():
     ap.add_argument("--size", type=int, default=None, help="override grid size")
     ap.add_argument("--batch", type=int, default=None, help="override instances per GPU")
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--cpu-sweeps", type=int, default=4, help="timed CPU sweeps per statement")
-    ap.add_argument("--traffic", default=None,
-                    help="JSON with PMC-derived HBM bytes per launch (default: newest profiles/*_traffic.json, "
-                         "written by tools/parse_rocprof.py from a rocprofv3 --pmc run of this workload)")
-    return ap.parse_args()
+    ap.add_argument("--no-config1", action="store_true", help="skip the config-1 (5x5) same-run timings")
+    ap.add_argument("--first-steps", type=int, default=FIRST_STEPS,
+                    help="steps from theta0 reported in first_steps (0: off)")
+    ap.add_argument("--cpu-sweeps", type=int, default=60, help="timed CPU sweeps per statement")
+    ap.add_argument("--profile", default=None,
+                    help="profiles/<tag>_summary.json of a rocprofv3 run of this workload (default: newest); its "
+                         "kernel average and PMC HBM bytes are reported beside the live figures")
+    return ap.parse_args(argv)
 
 
-def _latest_traffic():
+def _latest(pattern):
     import glob
-    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "r*_traffic.json")))
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", pattern)))
     return files[-1] if files else None
 
 
 CPU_DENSE_MAX = 128   # larger dense fp64 tables do not fit host RAM (256x256: 137 GB); extrapolate
 
 
-def cpu_baseline(size, p_slip, k_b, k_f, n_sweeps, causal=False):
-    """Time the reference's dense statements on one instance (oracle restatement).
-
-    Above 128x128 the dense table does not fit in host memory: the statements are
-    timed at 128x128 and scaled by the dense work ratio (S / 16384)^2, labelled
-    "extrapolated" (SURVEY.md 8(d))."""
-    if size > CPU_DENSE_MAX:
-        base = cpu_baseline(CPU_DENSE_MAX, p_slip, k_b, k_f, n_sweeps, causal)
-        ratio = (size * size / float(CPU_DENSE_MAX * CPU_DENSE_MAX)) ** 2
-        base["value"] /= ratio
-        base["sample"] = (f"extrapolated: {size}x{size} dense fp64 does not fit host RAM; per-sweep and copy "
-                          f"times measured at {CPU_DENSE_MAX}x{CPU_DENSE_MAX} x (S ratio)^2 = {ratio:.0f}, with "
-                          f"this run's K_b={k_b:.0f}, K_f={k_f:.0f} -- " + base["sample"])
-        return base
-    sys.path.insert(0, os.path.join(ROOT, "oracle"))
-    import maxent_oracle as O
+def blas_threads():
     try:
         from threadpoolctl import threadpool_info
-        threads = max([i.get("num_threads", 1) for i in threadpool_info() if i.get("user_api") == "blas"] or [1])
+        return max([i.get("num_threads", 1) for i in threadpool_info() if i.get("user_api") == "blas"] or [1])
     except Exception:
-        threads = int(os.environ.get("OMP_NUM_THREADS", "1"))
+        return int(os.environ.get("OMP_NUM_THREADS", "1"))
+
+
+def cpu_sweep_times(size, p_slip, n_sweeps, causal=False):
+    """Seconds per sweep of the reference's dense statements on one instance
+    (oracle restatement): forward maxent.py:109-112, backward :155-156 (or soft
+    VI :329-338), and one call's table copies maxent.py:98-102, 143 (320).
+
+    Above 128x128 the dense table does not fit in host memory: the statements
+    are timed at 128x128 and scaled by the dense work ratio (S / 16384)^2."""
+    if size > CPU_DENSE_MAX:
+        t = cpu_sweep_times(CPU_DENSE_MAX, p_slip, n_sweeps, causal)
+        ratio = (size * size / float(CPU_DENSE_MAX * CPU_DENSE_MAX)) ** 2
+        t.update(t_f=t["t_f"] * ratio, t_b=t["t_b"] * ratio, t_copy=t["t_copy"] * ratio, ratio=ratio,
+                 extrapolated_from=CPU_DENSE_MAX)
+        return t
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import maxent_oracle as O
     S = size * size
     t0 = time.perf_counter()
     P = O.icy_gridworld_table(size, p_slip)
     t_build = time.perf_counter() - t0
     terminal = [S - 1]
-    # per-call preprocessing of the forward and backward passes (maxent.py:98-102, 143)
     t0 = time.perf_counter()
     p = np.copy(P)
     p[terminal, :, :] = 0.0
@@ -123,6 +139,8 @@ def cpu_baseline(size, p_slip, k_b, k_f, n_sweeps, causal=False):
     d = rng.uniform(0.0, 1.0, S)
     er = np.exp(np.ones(S))
     zs = rng.uniform(0.0, 1.0, S)
+    phi = O.terminal_reward(terminal, S)
+    r = np.ones(S)
 
     def fwd_sweep(d):   # maxent.py:109-112
         parts = [fw[a].T.dot(pi[:, a] * d) for a in range(4)]
@@ -131,10 +149,7 @@ def cpu_baseline(size, p_slip, k_b, k_f, n_sweeps, causal=False):
 
     def bwd_sweep(zs):  # maxent.py:155-156
         za = np.array([er * bw[a].dot(zs) for a in range(4)]).T
-        return za.sum(axis=1)
-
-    phi = O.terminal_reward(terminal, S)
-    r = np.ones(S)
+        return za.sum(axis=1) * 1e-3
 
     def soft_sweep(v):  # maxent.py:329-338
         q = np.array([r + DISCOUNT * bw[a].dot(v) for a in range(4)]).T
@@ -145,34 +160,88 @@ def cpu_baseline(size, p_slip, k_b, k_f, n_sweeps, causal=False):
         np.max(np.abs(nv - v))
         return nv
 
+    back = soft_sweep if causal else bwd_sweep
     if causal:
-        bwd_sweep = soft_sweep   # noqa: F811 (same timing loop below)
         zs = -1e200 * np.ones(S)
-
     for _ in range(2):
         fwd_sweep(d)
-        bwd_sweep(zs)
+        back(zs)
     t0 = time.perf_counter()
     for _ in range(n_sweeps):
         _, d = fwd_sweep(d)
     t_f = (time.perf_counter() - t0) / n_sweeps
     t0 = time.perf_counter()
     for _ in range(n_sweeps):
-        zs = bwd_sweep(zs) if causal else bwd_sweep(zs) * 1e-3
+        zs = back(zs)
     t_b = (time.perf_counter() - t0) / n_sweeps
-    t_step = k_b * t_b + k_f * t_f + t_copy
-    return {
-        "value": 1.0 / t_step,
-        "unit": "instance-steps/s",
-        "cores": int(threads),
-        "host_cpu_count": os.cpu_count(),
-        "kind": "port",
-        "sample": (f"dense fp64 {size}x{size} (S={S}, A=4), one instance: {n_sweeps} timed sweeps each of "
-                   f"maxent.py:109-112 (forward, {t_f * 1e3:.1f} ms) and "
-                   f"{':329-338 (soft VI' if causal else ':155-156 (backward'}, {t_b * 1e3:.1f} ms) "
-                   f"+ one call's copies maxent.py:98-102,{320 if causal else 143} ({t_copy:.2f} s); step = K_b*t_b + K_f*t_f + t_copy "
-                   f"with this run's K_b={k_b:.0f}, K_f={k_f:.0f}; table build {t_build:.1f} s untimed"),
-    }
+    return {"t_f": t_f, "t_b": t_b, "t_copy": t_copy, "t_build": t_build, "n_sweeps": n_sweeps, "size": size,
+            "causal": causal, "ratio": 1.0, "extrapolated_from": None}
+
+
+def cpu_baseline_from(t, k_b, k_f):
+    """instance-steps/s of the timed statements at this run's mean sweep counts:
+    one step = K_b * t_b + K_f * t_f + t_copy."""
+    t_step = k_b * t["t_b"] + k_f * t["t_f"] + t["t_copy"]
+    S = t["size"] * t["size"]
+    sample = (f"dense fp64 {t['size']}x{t['size']} (S={S}, A=4), one instance: {t['n_sweeps']} timed sweeps "
+              f"each of maxent.py:109-112 (forward, {t['t_f'] / t['ratio'] * 1e3:.1f} ms) and "
+              f"{':329-338 (soft VI' if t['causal'] else ':155-156 (backward'}, "
+              f"{t['t_b'] / t['ratio'] * 1e3:.1f} ms) + one call's copies maxent.py:98-102,"
+              f"{320 if t['causal'] else 143} ({t['t_copy'] / t['ratio']:.2f} s); step = K_b*t_b + K_f*t_f + "
+              f"t_copy with this run's K_b={k_b:.0f}, K_f={k_f:.0f} (means over instances); table build "
+              f"{t['t_build']:.1f} s untimed")
+    if t["extrapolated_from"]:
+        sample = (f"extrapolated: the dense fp64 table does not fit host RAM; per-sweep and copy times "
+                  f"measured at {t['extrapolated_from']}x{t['extrapolated_from']} x (S ratio)^2 = "
+                  f"{t['ratio']:.0f} -- " + sample)
+    return {"value": 1.0 / t_step, "unit": "instance-steps/s", "cores": int(blas_threads()),
+            "host_cpu_count": os.cpu_count(), "kind": "port", "sample": sample}
+
+
+def cpu_baseline(size, p_slip, k_b, k_f, n_sweeps, causal=False):
+    return cpu_baseline_from(cpu_sweep_times(size, p_slip, n_sweeps, causal), k_b, k_f)
+
+
+def config1_timings(device_runs=True):
+    """BASELINE config 1 (src/main.py: IcyGridWorld(5, 0.2), 200 demonstrations,
+    identity features, ExpSga(linear_decay(0.2)), theta0 = 1): the full irl
+    (maxent.py:196-255) and irl_causal (discount 0.7, maxent.py:383-453) runs on
+    the device drop-in and on the CPU port (oracle, the reference's numpy
+    statements), both timed here.  The 200 demonstrations are the reference's
+    own (tests/golden/config1.npz, np.random.seed(0))."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import maxent_oracle as O
+    z = np.load(os.path.join(ROOT, "tests", "golden", "config1.npz"))
+    P, feats = z["p_transition"], np.identity(25)
+    tjs, o = [], 0
+    for n in z["traj_lens"]:
+        tjs.append(O.Trajectory([tuple(int(v) for v in row) for row in z["traj_flat"][o:o + n]]))
+        o += n
+    out = {"workload": "BASELINE config 1: src/main.py 5x5 IcyGridWorld, 200 demos, full runs to eps=1e-4",
+           "cpu_cores": int(blas_threads())}
+    runs = {"irl": lambda m, opt: m.irl(P, feats, [24], tjs, opt, O.Constant(1.0)),
+            "irl_causal": lambda m, opt: m.irl_causal(P, feats, [24], tjs, opt, O.Constant(1.0), DISCOUNT)}
+    import maxent as M   # the device drop-in (irl-maxent_amd/maxent.py)
+    for name, fn in runs.items():
+        rec = {}
+        if device_runs:
+            fn(M, O.ExpSga(lr=O.linear_decay(0.2)))          # warm-up (table upload, kernel load)
+            opt = O.ExpSga(lr=O.linear_decay(0.2))
+            t0 = time.perf_counter()
+            fn(M, opt)
+            rec["gpu_dropin_s"] = time.perf_counter() - t0
+            rec["steps"] = opt.k
+            rec["gpu_dropin_steps_per_s"] = opt.k / rec["gpu_dropin_s"]
+        opt = O.ExpSga(lr=O.linear_decay(0.2))
+        t0 = time.perf_counter()
+        _, k = fn(O, opt)                                    # the oracle's loops return (reward, steps)
+        rec["cpu_port_s"] = time.perf_counter() - t0
+        rec["cpu_port_steps"] = k
+        rec["cpu_port_steps_per_s"] = k / rec["cpu_port_s"]
+        if device_runs:
+            rec["speedup_vs_cpu"] = rec["cpu_port_s"] / rec["gpu_dropin_s"]
+        out[name] = rec
+    return out
 
 
 def stream_copy_gbs(dev, nbytes=1 << 30, reps=5):
@@ -194,28 +263,67 @@ def stream_copy_gbs(dev, nbytes=1 << 30, reps=5):
     return gbs
 
 
-def rank_env():
-    return int(os.environ.get("RANK", "0"))
+# ---------------------------------------------------------------------------
+# timing core (device-independent: tests drive it with stub steps over gloo)
+# ---------------------------------------------------------------------------
+
+def timed_steps(step, steps, warmup, barrier, sync, clock=time.perf_counter):
+    """W untimed warm-up steps, then exactly K steps bracketed by barrier + sync
+    on both sides.  ``step(i, timed)`` runs step i (0-based from theta0).
+    Returns (elapsed seconds of the K timed steps, per-step seconds of all
+    W + K steps -- each step ends with a sync, so the per-step clock is exact)."""
+    per_step = []
+    for i in range(warmup):
+        t = clock()
+        step(i, False)
+        sync()
+        per_step.append(clock() - t)
+    sync()
+    barrier()
+    sync()
+    t0 = clock()
+    for i in range(warmup, warmup + steps):
+        t = clock()
+        step(i, True)
+        sync()
+        per_step.append(clock() - t)
+    sync()
+    barrier()
+    sync()
+    return clock() - t0, per_step
 
 
-def main():
-    args = parse()
+def headline(elapsed_max, per_gpu, world, steps):
+    """(value, ms_per_step): whole-job instance-steps/s over the slowest rank's time."""
+    return per_gpu * world * steps / elapsed_max, elapsed_max / steps * 1e3
+
+
+def kernel_name(mode, plan, width):
+    """Symbol of the cluster_kernel instantiation a plan runs (cluster.hip)."""
+    return f"void irlmx::cluster_kernel<{mode}, {plan['spt']}, {width}, {plan['layout']}, {plan['threads']}>" \
+           f"(irlmx::ClusterArgs)"
+
+
+def main(argv=None):
+    args = parse(argv)
     import torch
     import torch.distributed as dist
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
-    if args.gpus != world and rank_env() == 0:
-        print(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world}; reporting {world} GPU(s)", file=sys.stderr)
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if args.gpus != world and rank == 0:
+        print(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world}; reporting {world} GPU(s)", file=sys.stderr)
     if world > 1:
-        dist.init_process_group(backend="nccl", device_id=torch.device("cuda", local))
+        # host-side group: only the timing barrier and the max-over-ranks travel
+        # (no data-path collective, SURVEY.md 8(e)) -- RCCL is not needed
+        dist.init_process_group(backend="gloo")
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
 
     import irlmx
     irlmx.load()          # prebuilt by __graft_entry__.build(); never compiled per rank
-    from irlmx import DeviceMDP, demos
+    from irlmx import DeviceMDP, demos, ops
     from irlmx.batch import BatchedMaxEnt
 
     size, per_gpu, desc, causal = CONFIGS[args.config]
@@ -236,24 +344,21 @@ def main():
     for i, b in enumerate(ids):
         e_f[i], p_0[i], _ = demos.sample(rv[i], size, terminal, 0, n=200, seed=1234 + int(b))
     irl = BatchedMaxEnt(mdp, e_f, p_0, terminal, causal=causal, discount=DISCOUNT if causal else None)
+    plans = {"backward": ops.execution_plan(mdp, "soft_backward" if causal else "backward"),
+             "forward": ops.execution_plan(mdp, "forward")}
     torch.cuda.synchronize()
 
     def barrier():
         if world > 1:
             dist.barrier()
 
-    for _ in range(args.warmup):
-        irl.step()
-    torch.cuda.synchronize()
-    barrier()
-    torch.cuda.synchronize()
-
     stream = torch.cuda.current_stream(dev)
+    n_all = args.warmup + args.steps
     ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True),
-           torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
+           torch.cuda.Event(enable_timing=True)) for _ in range(max(n_all, args.first_steps))]
     sweeps, bsweeps = [], []
-    t0 = time.perf_counter()
-    for i in range(args.steps):
+
+    def step(i, timed):
         e0, e1, e2 = ev[i]
         e0.record(stream)
         pi = irl.backward()
@@ -262,39 +367,78 @@ def main():
         e2.record(stream)
         irl.update(svf)
         sweeps.append(iters)
-        if causal:
-            bsweeps.append(irl.last_backward_sweeps)
-    torch.cuda.synchronize()
-    barrier()
-    torch.cuda.synchronize()
-    elapsed = time.perf_counter() - t0
+        bsweeps.append(irl.last_backward_sweeps if causal else torch.full_like(iters, 2 * S))
 
+    elapsed, per_step = timed_steps(step, args.steps, args.warmup, barrier, torch.cuda.synchronize)
     elapsed_max = max_over_ranks(elapsed, dev)
+    value, ms_per_step = headline(elapsed_max, per_gpu, world, args.steps)
 
-    k_f = torch.stack(sweeps).to(torch.float64)           # [steps, B]
-    # backward sweeps per instance and step: 2S-1 collapsed + 1 (maxent.py:151-156), or soft VI's count
-    k_b = torch.stack(bsweeps).to(torch.float64) if causal else torch.full_like(k_f, float(2 * S))
-    t_bwd = sum(e0.elapsed_time(e1) for e0, e1, _ in ev) * 1e-3
-    t_fwd = sum(e1.elapsed_time(e2) for _, e1, e2 in ev) * 1e-3
-    # SURVEY 8(d) algorithmic bytes: per instance and sweep 152*S (backward), 168*S (forward)
-    bwd_bytes = BYTES_BWD * S * float(k_b.sum())
-    fwd_bytes = BYTES_FWD * S * float(k_f.sum())
-    kern = {"backward": {"bytes": bwd_bytes, "seconds": t_bwd, "launches": args.steps,
-                         "flop": (FLOP_SOFT * S * float(k_b.sum()) if causal
-                                  else FLOP_BWD * S * float(2 * S - 1) * per_gpu * args.steps)},
-            "forward": {"bytes": fwd_bytes, "seconds": t_fwd, "launches": args.steps,
+    # steps 1..first_steps from theta0 (after the timed region: never inside it)
+    n_first = args.first_steps
+    for i in range(n_all, n_first):
+        t = time.perf_counter()
+        step(i, False)
+        torch.cuda.synchronize()
+        per_step.append(time.perf_counter() - t)
+
+    k_f_all = torch.stack(sweeps).to(torch.float64).cpu().numpy()      # [steps run, B]
+    k_b_all = torch.stack(bsweeps).to(torch.float64).cpu().numpy()
+    timed = slice(args.warmup, n_all)
+    k_f, k_b = k_f_all[timed], k_b_all[timed]
+    t_bwd = sum(ev[i][0].elapsed_time(ev[i][1]) for i in range(args.warmup, n_all)) * 1e-3
+    t_fwd = sum(ev[i][1].elapsed_time(ev[i][2]) for i in range(args.warmup, n_all)) * 1e-3
+    bwd_flop = (FLOP_SOFT if causal else FLOP_BWD) * S * float((k_b - (0 if causal else 1)).sum())
+    kern = {"backward": {"bytes": (BYTES_SOFT if causal else BYTES_BWD) * S * float(k_b.sum()), "seconds": t_bwd,
+                         "launches": args.steps, "flop": bwd_flop},
+            "forward": {"bytes": BYTES_FWD * S * float(k_f.sum()), "seconds": t_fwd, "launches": args.steps,
                         "flop": FLOP_FWD * S * float(k_f.sum())}}
     dom = max(kern, key=lambda k: kern[k]["seconds"])
-    achieved = kern[dom]["bytes"] / kern[dom]["seconds"] / 1e9
+    kd = kern[dom]
+    launch_s = kd["seconds"] / kd["launches"]
+    achieved = kd["flop"] / kd["seconds"] / 1e12
     if rank == 0:
+        dplan = plans[dom]
+        kname = kernel_name(1 if dom == "backward" else 0, dplan, size) if dplan["shape"] == "cluster" else None
+        roof = {
+            "bound": "fp64-valu", "kernel": kname or f"{dom} pass ({dplan['shape']} shape)",
+            "achieved": achieved, "peak": FP64_PEAK_TFS, "unit": "TFLOP/s", "frac": achieved / FP64_PEAK_TFS,
+            "traffic": None,
+            "flop_per_launch": kd["flop"] / kd["launches"], "launch_ms": launch_s * 1e3,
+            "frac_of_fma_loop": achieved / FP64_LOOP_TFS,
+            "note": ("binding resource = the fp64 VALU: every sweep is a chain of fp64 FMAs on registers/LDS "
+                     "(10 flop per state for the collapsed 5-point backward stencil, 11 forward, 44 soft VI); "
+                     "achieved = algorithmic flop per launch / average launch time (HIP events on the launch "
+                     "stream); peak = MI355X FP64 spec; frac_of_fma_loop = vs an independent-FMA loop measured "
+                     "on the box (tools/diag/dfma_rate.hip, 54.8 TFLOP/s at the clock fp64 load holds)"),
+            # SURVEY 8(d)'s streamed-ELL bytes for the same sweeps, against the PMC-measured HBM bytes:
+            # the state and weights stay on chip across sweeps, HBM carries the halo exchanges
+            "algorithmic_bytes_per_launch": kd["bytes"] / kd["launches"],
+        }
+        ppath = args.profile or _latest("r*_summary.json")
+        default_cfg = not args.size and not args.batch
+        if ppath and os.path.exists(ppath) and default_cfg:
+            prof = json.load(open(ppath))
+            src = os.path.relpath(ppath, ROOT)
+            k = prof.get("kernels", {}).get(kname) if kname else None
+            if k and prof.get("config", "c3") == args.config:
+                roof["rocprof_avg_ms"] = k["avg_ms"]
+                roof["frac_rocprof"] = kd["flop"] / kd["launches"] / (k["avg_ms"] * 1e-3) / 1e12 / FP64_PEAK_TFS
+                roof["rocprof_source"] = f"{src}: rocprofv3 --kernel-trace --stats average of {kname}"
+            tr = prof.get("traffic", {}).get(dom)
+            if tr and tr.get("kernel") == kname and prof.get("config", "c3") == args.config:
+                roof["traffic"] = tr["hbm_bytes_per_launch"]
+                roof["traffic_source"] = (f"{src}: FETCH_SIZE + WRITE_SIZE (KiB x 1024) of one {dom} dispatch, "
+                                          f"separate --pmc passes")
+                roof["hbm_frac"] = tr["hbm_bytes_per_launch"] / launch_s / 1e9 / HBM_PEAK_GBS
+                roof["onchip_reuse_factor"] = roof["algorithmic_bytes_per_launch"] / tr["hbm_bytes_per_launch"]
         out = {
             "metric": "IRL gradient steps/sec (VI + SVF sweep), NxN grid batch B",
-            "value": B_total * args.steps / elapsed_max,
+            "value": value,
             "unit": "instance-steps/s",
             "n_gpus": world,
             "steps": args.steps,
             "warmup": args.warmup,
-            "ms_per_step": elapsed_max / args.steps * 1e3,
+            "ms_per_step": ms_per_step,
             "higher_is_better": True,
             "scaling": "weak",
             "vs_baseline": None,
@@ -303,45 +447,38 @@ def main():
             "config": {"workload": desc, "grid": f"{size}x{size}", "n_states": S, "n_actions": 4,
                        "batch_per_gpu": per_gpu, "global_batch": B_total, "eps_svf": 1e-5,
                        "parallelism": f"instances sharded over {world} GPU(s), no collective"},
+            "plans": plans,
             "sweeps": {"backward_per_step": float(k_b.mean()), "forward_mean": float(k_f.mean()),
                        "forward_max": float(k_f.max())},
             "phase_s": {"backward": t_bwd, "forward": t_fwd},
-            "roofline": {"bound": "hbm", "kernel": f"{dom} pass (one launch per step covers every instance "
-                                                    f"and sweep)", "achieved": achieved,
-                         "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS,
-                         "traffic": None,
-                         "bytes_per_launch": kern[dom]["bytes"] / kern[dom]["launches"],
-                         "launch_ms": kern[dom]["seconds"] / kern[dom]["launches"] * 1e3,
-                         "note": "achieved = SURVEY 8(d) algorithmic bytes (152*S backward / 168*S forward per "
-                                 "instance-sweep) x sweeps / kernel time (HIP events on the launch stream); frac > 1: "
-                                 "the state vectors and weights stay on chip across sweeps (LDS + registers), "
-                                 "HBM only sees halo exchanges"},
-            "compute_roofline": {
-                "bound": "fp64-valu", "kernel": dom,
-                "achieved": kern[dom]["flop"] / kern[dom]["seconds"] / 1e12, "peak": FP64_PEAK_TFS,
-                "unit": "TFLOP/s", "frac": kern[dom]["flop"] / kern[dom]["seconds"] / 1e12 / FP64_PEAK_TFS,
-                "frac_of_fma_loop": kern[dom]["flop"] / kern[dom]["seconds"] / 1e12 / FP64_LOOP_TFS,
-                "flop_per_launch": kern[dom]["flop"] / kern[dom]["launches"],
-                "note": "the binding resource: every sweep is a chain of fp64 FMAs on the VALU (10 flop per "
-                        "state for the collapsed 5-point stencil, 11 forward); peak = MI355X FP64 spec, "
-                        "frac_of_fma_loop = vs a pure independent-FMA loop measured on the box "
-                        "(tools/diag/dfma_rate.hip, 54.8 TFLOP/s at the clock fp64 load holds)"},
-            "per_kernel": {k: {"achieved_GBs": v["bytes"] / v["seconds"] / 1e9, "ms_per_launch": v["seconds"] /
-                               v["launches"] * 1e3, "achieved_TFLOPs": v["flop"] / v["seconds"] / 1e12}
+            "roofline": roof,
+            "per_kernel": {k: {"ms_per_launch": v["seconds"] / v["launches"] * 1e3,
+                               "achieved_TFLOPs": v["flop"] / v["seconds"] / 1e12,
+                               "algorithmic_GBs": v["bytes"] / v["seconds"] / 1e9}
                            for k, v in kern.items()},
         }
+        if n_first:
+            t_first = sum(per_step[:n_first])
+            out["first_steps"] = {
+                "steps": n_first, "seconds": t_first, "instance_steps_per_s": per_gpu * n_first / t_first,
+                "step1_ms": per_step[0] * 1e3,
+                "forward_sweeps_mean": [float(v) for v in k_f_all[:n_first].mean(axis=1)],
+                "note": ("steps 1..N of irl from theta0 = 1 on this GPU's instances, each timed to its own sync "
+                         "(the warm-up and timed steps are the first W + K); step 1's forward runs to convergence "
+                         "from the unit reward (~360k sweeps at 128x128)")}
         out["roofline"]["stream_copy_GBs"] = stream_copy_gbs(dev)
-        tpath = args.traffic or _latest_traffic()
-        if tpath and os.path.exists(tpath) and args.config == "c3" and not args.size and not args.batch:
-            tr = json.load(open(tpath)).get(dom)
-            if tr:
-                out["roofline"]["traffic"] = tr["hbm_bytes_per_launch"]
-                out["roofline"]["traffic_source"] = (f"{os.path.relpath(tpath, ROOT)}: FETCH_SIZE + WRITE_SIZE "
-                                                     f"(KiB x 1024) of one {dom} dispatch, separate --pmc passes")
         if world == 1 and not args.no_cpu_baseline:
-            out["cpu_baseline"] = cpu_baseline(size, float(slips[0]), float(k_b[:, 0].mean()),
-                                               float(k_f[:, 0].mean()), args.cpu_sweeps, causal)
+            t = cpu_sweep_times(size, float(slips[0]), args.cpu_sweeps, causal)
+            out["cpu_baseline"] = cpu_baseline_from(t, float(k_b.mean()), float(k_f.mean()))
             out["speedup_vs_cpu"] = out["value"] / out["cpu_baseline"]["value"]
+            if n_first:
+                kb_first = k_b_all[:n_first].mean(axis=1)
+                kf_first = k_f_all[:n_first].mean(axis=1)
+                t_cpu = float(np.sum(kb_first * t["t_b"] + kf_first * t["t_f"] + t["t_copy"]))
+                out["first_steps"]["cpu_baseline_instance_steps_per_s"] = n_first / t_cpu
+                out["first_steps"]["speedup_vs_cpu"] = out["first_steps"]["instance_steps_per_s"] * t_cpu / n_first
+            if not args.no_config1:
+                out["config1"] = config1_timings()
         print(json.dumps(out), flush=True)
     if world > 1:
         dist.destroy_process_group()

@@ -141,6 +141,23 @@ int irlmx_value_iteration(const irlmx_mdp* mdp, const double* reward, double dis
                           int32_t* status, void* workspace, size_t workspace_bytes, void* stream);
 
 /*
+ * Execution plan a call of `op` (IRLMX_OP_*) on this model would run, without
+ * running it (diagnostics and tests: the bench and the parity tests assert that
+ * they exercise the same kernel instantiation).  No reference counterpart.
+ * Writes plan[IRLMX_PLAN_LEN]:
+ *   [0] shape (IRLMX_SHAPE_*)   [1] R rows per tile   [2] G ghost rows
+ *   [3] C tiles per instance   [4] instances per launch   [5] states per lane
+ *   [6] in-tile layout (0 per state, 1 pair rows, 2 column pairs, 3 column quads)
+ *   [7] threads per workgroup  [8] sequential launches   [9] LDS bytes
+ * Cluster fields are 0 for the other shapes.  Depends on the current device.
+ */
+#define IRLMX_PLAN_LEN 10
+#define IRLMX_SHAPE_FUSED 0   /* one workgroup per instance for the whole loop */
+#define IRLMX_SHAPE_CLUSTER 1 /* persistent row tiles with halo exchanges */
+#define IRLMX_SHAPE_SWEEP 2   /* one launch per sweep */
+int irlmx_execution_plan(const irlmx_mdp* mdp, int32_t op, int64_t* plan);
+
+/*
  * Policy extraction from a value function -- replaces
  * solver.optimal_policy_from_value (src/solver.py:107-124: argmax over the
  * values of the intended successors, first index on ties and NaN counted as

@@ -898,6 +898,35 @@ extern "C" size_t irlmx_workspace_bytes(const irlmx_mdp* mdp, int32_t op) {
   return carve(make_model(mdp), op, nullptr).total;
 }
 
+extern "C" int irlmx_execution_plan(const irlmx_mdp* mdp, int32_t op, int64_t* plan) {
+  if (int rc = validate(mdp)) return rc;
+  if (!plan) { set_error("plan is NULL"); return IRLMX_EINVAL; }
+  if (op < IRLMX_OP_BACKWARD || op > IRLMX_OP_VALUE_ITERATION) { set_error("unknown op %d", op); return IRLMX_EINVAL; }
+  const Model m = make_model(mdp);
+  for (int i = 0; i < IRLMX_PLAN_LEN; ++i) plan[i] = 0;
+  FusedShape fs;
+  if (fused_shape(m, op, &fs)) {
+    plan[0] = IRLMX_SHAPE_FUSED;
+    plan[5] = fs.spt;
+    plan[7] = fs.threads;
+    plan[8] = 1;
+    plan[9] = (int64_t)fused_lds(m);
+    return 0;
+  }
+  ClusterPlan cp;
+  const int mode = op == IRLMX_OP_FORWARD ? kModeFwd : kModeBwd;
+  if (m.stencil && (op == IRLMX_OP_FORWARD || op == IRLMX_OP_BACKWARD) && cluster_plan(m.W, m.H, m.B, mode, &cp)) {
+    plan[0] = IRLMX_SHAPE_CLUSTER;
+    plan[1] = cp.R; plan[2] = cp.G; plan[3] = cp.C; plan[4] = cp.per_launch; plan[5] = cp.spt;
+    plan[6] = cp.pair; plan[7] = cp.nt; plan[8] = (m.B + cp.per_launch - 1) / cp.per_launch;
+    plan[9] = (int64_t)cp.lds;
+    return 0;
+  }
+  plan[0] = IRLMX_SHAPE_SWEEP;
+  plan[7] = kSweepThreads;
+  return 0;
+}
+
 extern "C" int irlmx_forward_svf(const irlmx_mdp* mdp, const double* p_initial, const uint8_t* terminal,
                                  const double* p_action, double eps, int64_t max_iter, double* svf,
                                  int64_t* iterations, int32_t* status, void* workspace,

@@ -66,6 +66,7 @@ SIGNATURES = {
     "irlmx_forward_svf": (ctypes.c_int, [_MDP, _P, _P, _P, _D, _I64, _P, _P, _P, _P, _SZ, _P]),
     "irlmx_soft_backward": (ctypes.c_int, [_MDP, _P, _P, _D, _D, _I64, _P, _P, _P, _P, _P, _SZ, _P]),
     "irlmx_value_iteration": (ctypes.c_int, [_MDP, _P, _D, _D, _I32, _I64, _P, _P, _P, _P, _SZ, _P]),
+    "irlmx_execution_plan": (ctypes.c_int, [_MDP, _I32, _P]),
     "irlmx_optimal_policy": (ctypes.c_int, [_P, _I32, _I32, _I32, _P, _P, _P]),
     "irlmx_stochastic_policy": (ctypes.c_int, [_P, _I32, _I32, _I32, _P, _P, _P]),
     "irlmx_build_icy_gridworld": (ctypes.c_int, [_I32, _P, _I32, _P, _P]),

@@ -12,18 +12,37 @@ import torch
 from . import _lib
 from .mdp import DeviceMDP
 
-_workspaces = {}
-
-
 def _workspace(mdp, op):
+    """Device workspace for one call, from torch's caching allocator.
+
+    Allocated per call on the current stream: the allocator hands a freed block
+    only to later work on the same stream (stream-ordered), so concurrent calls
+    from other host threads or on other streams never share a workspace that an
+    in-flight kernel still uses -- the stream / thread safety include/irlmx.h
+    states for the C ABI."""
     lib = _lib.load()
     n = int(lib.irlmx_workspace_bytes(mdp.struct(), op))
-    key = (mdp.device, op)
-    ws = _workspaces.get(key)
-    if ws is None or ws.numel() < n:
-        ws = torch.empty(max(n, 256), dtype=torch.uint8, device=mdp.device)
-        _workspaces[key] = ws
-    return ws, n
+    return torch.empty(max(n, 256), dtype=torch.uint8, device=mdp.device), n
+
+
+PLAN_FIELDS = ("shape", "R", "G", "C", "per_launch", "spt", "layout", "threads", "launches", "lds_bytes")
+SHAPES = {0: "fused", 1: "cluster", 2: "sweep"}
+_OPS = {"backward": _lib.OP_BACKWARD, "forward": _lib.OP_FORWARD, "soft_backward": _lib.OP_SOFT_BACKWARD,
+        "value_iteration": _lib.OP_VALUE_ITERATION}
+
+
+def execution_plan(mdp, op):
+    """The kernel plan a call of ``op`` ("backward", "forward", "soft_backward",
+    "value_iteration") on ``mdp`` runs on the current device (irlmx_execution_plan):
+    shape, tile rows R, ghost rows G, tiles per instance C, instances per launch,
+    states per lane, in-tile layout, threads, sequential launches, LDS bytes."""
+    import ctypes
+    lib = _lib.load()
+    buf = (ctypes.c_int64 * len(PLAN_FIELDS))()
+    _lib.check(lib.irlmx_execution_plan(mdp.struct(), _OPS[op], buf), "execution_plan")
+    plan = dict(zip(PLAN_FIELDS, [int(v) for v in buf]))
+    plan["shape"] = SHAPES[plan["shape"]]
+    return plan
 
 
 def _f64(x, mdp, shape):
@@ -144,5 +163,5 @@ def stochastic_policy(successor, weighted_value):
     return out
 
 
-__all__ = ["DeviceMDP", "terminal_mask", "backward_maxent", "forward_svf", "soft_backward",
+__all__ = ["DeviceMDP", "execution_plan", "terminal_mask", "backward_maxent", "forward_svf", "soft_backward",
            "value_iteration", "optimal_policy", "stochastic_policy"]

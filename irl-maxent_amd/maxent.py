@@ -33,9 +33,11 @@ def _rescale():
 
 
 def _model(p_transition):
+    """The device model of ``p_transition`` (uploaded once per array, see
+    DeviceMDP.resident; the reference re-copies it per call, maxent.py:98-102, 143, 320)."""
     if isinstance(p_transition, DeviceMDP):
         return p_transition
-    return DeviceMDP.from_dense(p_transition)
+    return DeviceMDP.resident(p_transition)
 
 
 def _host(t):

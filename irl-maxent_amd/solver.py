@@ -15,7 +15,7 @@ __all__ = ["value_iteration", "stochastic_value_iteration", "optimal_policy_from
 
 
 def _model(p):
-    return p if isinstance(p, DeviceMDP) else DeviceMDP.from_dense(p)
+    return p if isinstance(p, DeviceMDP) else DeviceMDP.resident(p)
 
 
 def value_iteration(p, reward, discount, eps=1e-3):

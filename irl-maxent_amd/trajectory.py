@@ -20,29 +20,41 @@ step selects the same successor.  Worlds may be the reference's (dense
 the host once): O(1) per step at any grid size.
 """
 
-from itertools import chain
+import operator
+from functools import partial
 
 import numpy as np
 
 
 class Trajectory:
-    """A trajectory of ``(state_from, action, state_to)`` transitions (trajectory.py:10-49)."""
+    """A demonstration: a list of ``(state_from, action, state_to)`` transitions
+    (the container of trajectory.py:10-49; the same accessors and string forms)."""
+
+    __slots__ = ("_steps",)
 
     def __init__(self, transitions):
-        self._t = transitions
+        self._steps = transitions
 
     def transitions(self):
-        return self._t
+        return self._steps
 
     def states(self):
-        """Visited states in order, the final state included (trajectory.py:38-46)."""
-        return map(lambda x: x[0], chain(self._t, [(self._t[-1][2], 0, 0)]))
+        """Iterator over the visited states in order, the final state included
+        (trajectory.py:33-43).  The final state is read at call time, so an empty
+        trajectory raises IndexError here, as the reference's does."""
+        final = self._steps[-1][2]
+
+        def visits():
+            for step in self._steps:
+                yield step[0]
+            yield final
+        return visits()
 
     def __repr__(self):
-        return "Trajectory({})".format(repr(self._t))
+        return f"Trajectory({self._steps!r})"
 
     def __str__(self):
-        return "{}".format(self._t)
+        return str(self._steps)
 
 
 # -- successor rows --------------------------------------------------------------
@@ -117,39 +129,44 @@ def _choice_sparse(idx, p):
 # -- generation --------------------------------------------------------------------
 
 def generate_trajectory(world, policy, start, final):
-    """One trajectory from ``start`` until a state in ``final`` (trajectory.py:52-85)."""
+    """One trajectory from ``start`` until a state in ``final`` (trajectory.py:52-87):
+    per step one policy call, then one successor draw."""
     rows = _rows(world)
+    steps = []
     state = start
-    trajectory = []
     while state not in final:
         action = policy(state)
-        next_s, next_p = rows.row(state, action)
-        next_state = _choice_sparse(next_s, next_p)
-        trajectory += [(state, action, next_state)]
-        state = next_state
-    return Trajectory(trajectory)
+        succ = _choice_sparse(*rows.row(state, action))
+        steps.append((state, action, succ))
+        state = succ
+    return Trajectory(steps)
 
 
 def generate_trajectories(n, world, policy, start, final):
-    """A generator of ``n`` trajectories (trajectory.py:88-128).  ``start``: a state,
-    a list of states (chosen uniformly), or a distribution over all states."""
-    start_states = np.atleast_1d(start)
+    """Lazily generate ``n`` trajectories (trajectory.py:90-128).  ``start``: one
+    state, a list of states (one drawn uniformly per trajectory), or a
+    distribution over all states (when it has one entry per state)."""
+    starts = np.atleast_1d(start)
 
-    def _generate_one():
-        if len(start_states) == world.n_states:
-            s = np.random.choice(range(world.n_states), p=start_states)
-        else:
-            s = np.random.choice(start_states)
-        return generate_trajectory(world, policy, s, final)
+    def draw_start():
+        if len(starts) == world.n_states:
+            return np.random.choice(world.n_states, p=starts)   # same single draw as choice(range(S), p)
+        return np.random.choice(starts)
 
-    return (_generate_one() for _ in range(n))
+    def trajectories():
+        for _ in range(n):
+            yield generate_trajectory(world, policy, draw_start(), final)
+    return trajectories()
 
 
 def policy_adapter(policy):
-    """Deterministic policy array -> ``state -> action`` (trajectory.py:131-145)."""
-    return lambda state: policy[state]
+    """Deterministic policy (array or map ``state -> action``) as a callable
+    (trajectory.py:131-147)."""
+    return partial(operator.getitem, policy)
 
 
 def stochastic_policy_adapter(policy):
-    """Stochastic policy ``[state, action]`` -> sampled ``state -> action`` (trajectory.py:148-166)."""
-    return lambda state: np.random.choice([*range(policy.shape[1])], p=policy[state, :])
+    """Stochastic policy ``[state, action]`` as a callable that samples an action
+    per call (trajectory.py:150-169)."""
+    n_actions = policy.shape[1]
+    return lambda state: np.random.choice(n_actions, p=policy[state, :])

@@ -12,7 +12,7 @@ import bench  # noqa: E402
 
 
 def test_configs_cover_baseline_rows():
-    # BASELINE.json configs 2-5 (config 1 is the 5x5 main.py run, timed by tools/diag/config1_timing.py)
+    # BASELINE.json configs 2-5 (config 1, the 5x5 main.py run, is timed by bench.config1_timings)
     assert set(bench.CONFIGS) == {"c2", "c3", "c4", "c5"}
     size, per_gpu, _, causal = bench.CONFIGS["c3"]
     assert (size, per_gpu, causal) == (128, 64, False)
@@ -35,3 +35,39 @@ def test_cpu_baseline_extrapolates_above_dense_limit(monkeypatch):
     assert big["sample"].startswith("extrapolated") and "(S ratio)^2 = 16" in big["sample"]
     # (S ratio)^2 = 16: the same statements timed again, divided by 16
     assert 0 < big["value"] < base["value"]
+
+
+def test_cpu_baseline_uses_mean_sweeps():
+    t = bench.cpu_sweep_times(6, 0.2, 1)
+    a = bench.cpu_baseline_from(t, 72, 100.0)
+    b = bench.cpu_baseline_from(t, 72, 300.0)
+    assert a["value"] > b["value"] > 0
+    assert abs(1.0 / b["value"] - 1.0 / a["value"] - 200.0 * t["t_f"]) < 1e-12
+    assert "means over instances" in a["sample"]
+
+
+def test_config1_cpu_leg():
+    out = bench.config1_timings(device_runs=False)
+    # the reference's step counts for src/main.py's problem (tests/golden/config1.npz)
+    assert out["irl"]["cpu_port_steps"] == 375 and out["irl_causal"]["cpu_port_steps"] == 419
+    assert out["irl"]["cpu_port_steps_per_s"] > 0
+
+
+def test_timed_steps_brackets_exactly_k_steps():
+    calls, log = [], []
+    clock_t = [0.0]
+
+    def clock():
+        return clock_t[0]
+
+    def step(i, timed):
+        calls.append((i, timed))
+        clock_t[0] += 1.0 + i
+
+    elapsed, per_step = bench.timed_steps(step, 3, 2, lambda: log.append("barrier"), lambda: log.append("sync"),
+                                          clock=clock)
+    assert calls == [(0, False), (1, False), (2, True), (3, True), (4, True)]
+    assert elapsed == 3.0 + 4.0 + 5.0 and per_step == [1.0, 2.0, 3.0, 4.0, 5.0]
+    assert log.count("barrier") == 2
+    v, ms = bench.headline(elapsed, 64, 2, 3)
+    assert v == 64 * 2 * 3 / 12.0 and ms == 4000.0

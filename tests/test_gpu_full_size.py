@@ -1,9 +1,10 @@
 """HIP path at the BASELINE configs' full grid sizes (needs an MI355X).
 
 128x128 (configs 3 and 5): the device's backward pass (2*S = 32,768 sweeps on
-the default cluster plan -- column-strip layout, 4 tiles per instance, halo
-exchanges, block-boundary rescaling) and a forward pass capped at 3,000
-sweeps, against the CPU oracle's sparse-operand restatement of the same
+the cluster plan the planner picks for two instances -- column-strip layout,
+R = 4 / G = 14 / C = 32 tiles per instance, halo exchanges, block-boundary
+rescaling; the bench's own B = 64 plan is tested in test_gpu_bench_plans.py)
+and a forward pass capped at 3,000 sweeps, against the CPU oracle's sparse-operand restatement of the same
 reference statements (oracle/maxent_oracle.py ``*_csr``, maxent.py:98-112,
 143-159), two instances with distinct slip probabilities.  The reference
 itself overflows to NaN beyond 12x12 (its unscaled backward), so the oracle

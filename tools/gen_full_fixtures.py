@@ -1,0 +1,132 @@
+#!/usr/bin/env python
+"""Converged full-size fixtures for the GPU parity tests (tests/golden/full_*.npz).
+
+The reference cannot reach these sizes (its unscaled backward is NaN beyond
+12x12 and its dense sweeps take hours at 128x128), so the expected values come
+from the CPU oracle's sparse-operand restatement (oracle/maxent_oracle.py
+``*_csr``), which tests/test_oracle_golden.py pins to the dense restatement and
+that one to the reference's own outputs.  Everything here runs in the build
+container only; the GPU box reads the .npz files.
+
+Workloads are exactly the bench's (bench.py CONFIGS, irlmx.shard.instance_slips,
+irlmx.demos.sample with seed 1234 + b):
+
+  full_c3.npz  128x128, B = 64: instances b = 0 and 63, the first 3 gradient
+               steps of irl (maxent.py:240-252) from theta = 1 -- step 1's
+               forward runs ~360k sweeps to convergence.
+  full_c4.npz  256x256, 32 instances per GPU: b = 0 and 31, the first 2 steps.
+               Vectors of 65,536 states are stored on a fixed subset of 4,096
+               states plus whole-vector sums (sum, sum |x|, max |x|).
+  full_c5.npz  128x128 causal (config 5): the forward pass to convergence on the
+               reference's own soft-VI policy (tests/golden/causal_128.npz), and
+               the first 2 irl_causal steps (maxent.py:437-450) of the bench's
+               c5 workload (one instance, discount 0.7).
+
+Usage: python tools/gen_full_fixtures.py [c3 c4 c5]   (~15 min on 8 cores)
+"""
+
+import os
+import sys
+import time
+from multiprocessing import Pool
+
+for v in ("OMP_NUM_THREADS", "OPENBLAS_NUM_THREADS", "MKL_NUM_THREADS"):
+    os.environ[v] = "1"
+
+import numpy as np  # noqa: E402
+
+ROOT = os.path.join(os.path.dirname(os.path.abspath(__file__)), "..")
+sys.path.insert(0, os.path.join(ROOT, "oracle"))
+sys.path.insert(0, os.path.join(ROOT, "irl-maxent_amd"))
+OUT = os.path.join(ROOT, "tests", "golden")
+
+import maxent_oracle as O  # noqa: E402
+from irlmx import demos    # noqa: E402  (the bench's own input generator: numpy only)
+
+SUBSET_MAX_S = 16384   # larger vectors are stored on a subset of states
+
+
+def subset(n_states, size, k=4096, seed=99):
+    rng = np.random.default_rng(seed)
+    pick = set(rng.choice(n_states, k - 8, replace=False).tolist())
+    pick |= {0, size - 1, n_states - size, n_states - 1, size, 2 * size - 1, n_states // 2, n_states // 2 + 1}
+    return np.array(sorted(pick))[:k]
+
+
+def pack(prefix, vec, idx, out):
+    vec = np.asarray(vec)
+    out[prefix + "_sum"] = np.array([vec.sum(), np.abs(vec).sum(), np.abs(vec).max()])
+    out[prefix] = vec if idx is None else vec[idx]
+
+
+def bench_instance(size, b, n_total):
+    slip = 0.1 + 0.2 * float(b) / n_total       # irlmx.shard.instance_slips
+    mats = O.icy_gridworld_csr(size, slip)
+    rv = O.stencil_row_val(mats, size)
+    n = size * size
+    e_f, p0, _ = demos.sample(rv, size, [n - 1], 0, n=200, seed=1234 + b)
+    return slip, mats, e_f, p0
+
+
+def job_irl(args):
+    cfg, size, n_total, b, n_steps, causal = args
+    t0 = time.time()
+    n = size * size
+    slip, mats, e_f, p0 = bench_instance(size, b, n_total)
+    res = O.irl_steps_csr(mats, e_f, p0, [n - 1], n_steps, causal=causal, discount=0.7 if causal else None)
+    idx = None if n <= SUBSET_MAX_S else subset(n, size)
+    out = {"slip": np.array(slip), "e_f": e_f, "p0": p0,
+           "k_f": np.array(res["k_f"]), "k_b": np.array(res["k_b"])}
+    if idx is not None:
+        out["idx"] = idx
+    for i in range(n_steps):
+        pack(f"svf{i}", res["svf"][i], idx, out)
+        pack(f"theta{i}", res["theta"][i], idx, out)
+    pi0 = res["pi"][0]
+    if idx is None:
+        out["pi0"] = pi0
+    else:
+        out["pi0"] = pi0[idx]
+        out["pi0_sum"] = np.array([pi0.sum(), np.abs(pi0).max()])
+    print(f"[{cfg} b={b}] k_f={res['k_f']} k_b={res['k_b']} {time.time() - t0:.0f}s", flush=True)
+    return cfg, b, out
+
+
+def job_c5_forward(_):
+    t0 = time.time()
+    z = np.load(os.path.join(OUT, "causal_128.npz"))
+    size = int(z["size"])
+    n = size * size
+    p0 = np.zeros(n)
+    p0[0] = 1.0
+    svf, k = O.forward_svf_csr(O.icy_gridworld_csr(size, 0.2), p0, [n - 1], z["pi"])
+    print(f"[c5 forward] k_f={k} {time.time() - t0:.0f}s", flush=True)
+    return "c5", "fwd", {"svf": svf, "k_f": np.array(k)}
+
+
+def main():
+    which = sys.argv[1:] or ["c3", "c4", "c5"]
+    jobs = []
+    if "c3" in which:
+        jobs += [(job_irl, ("c3", 128, 64, b, 3, False)) for b in (0, 63)]
+    if "c4" in which:
+        jobs += [(job_irl, ("c4", 256, 32, b, 2, False)) for b in (0, 31)]
+    if "c5" in which:
+        jobs += [(job_c5_forward, None), (job_irl, ("c5", 128, 1, 0, 2, True))]
+    with Pool(len(jobs)) as pool:
+        res = [pool.apply_async(f, (a,)) for f, a in jobs]
+        res = [r.get() for r in res]
+    files = {}
+    for cfg, key, out in res:
+        d = files.setdefault(cfg, {})
+        for k, v in out.items():
+            d[f"{key}__{k}" if key != "fwd" else f"fwd__{k}"] = v
+    for cfg, d in files.items():
+        d["instances"] = np.array(sorted({int(k.split("__")[0]) for k in d if k.split("__")[0].isdigit()}))
+        path = os.path.join(OUT, f"full_{cfg}.npz")
+        np.savez_compressed(path, **d)
+        print("wrote", path, os.path.getsize(path), "bytes")
+
+
+if __name__ == "__main__":
+    main()
