@@ -39,6 +39,7 @@ extern "C" {
 /* transition-table layouts (see irlmx_mdp) */
 #define IRLMX_LAYOUT_STENCIL5 1 /* grid-local: self, +x, -x, +y, -y on a width x height grid */
 #define IRLMX_LAYOUT_ELL 2      /* generic sparse: k_row target slots per state */
+#define IRLMX_LAYOUT_DENSE 3    /* dense rows: per-action S x S matrices (non-grid, dense P) */
 
 /* return codes */
 #define IRLMX_SUCCESS 0
@@ -68,6 +69,12 @@ extern "C" {
  *  column form (used by the forward SVF pass, ELL only; STENCIL5 derives it):
  *    col_idx[b'][k][t] = source state s of slot k of target t,
  *    col_val[b'][a][k][t] = P[s, t, a].
+ *  dense form (DENSE: most (s, t) pairs nonzero, where ELL would gather ~S slots
+ *  per state):
+ *    row_val[b'][a][s][t] = P[s, t, a]     the reference's slices P[:, :, a]
+ *                                          (maxent.py:102, 143, 320), row-major
+ *    col_val[b'][s][t]    = sum_a P[s, t, a]  (action-summed, for the backward)
+ *    row_idx, col_idx unused; k_row = k_col = n_states.
  *  b' = 0 when `shared` is nonzero (one table for all B instances), else b.
  */
 typedef struct irlmx_mdp {
@@ -155,6 +162,8 @@ int irlmx_value_iteration(const irlmx_mdp* mdp, const double* reward, double dis
 #define IRLMX_SHAPE_FUSED 0   /* one workgroup per instance for the whole loop */
 #define IRLMX_SHAPE_CLUSTER 1 /* persistent row tiles with halo exchanges */
 #define IRLMX_SHAPE_SWEEP 2   /* one launch per sweep */
+#define IRLMX_SHAPE_DENSE 3   /* DENSE layout: one launch per sweep, matrix rows streamed per instance */
+#define IRLMX_SHAPE_DENSE_GEMM 4 /* DENSE, shared table: the backward sweep as one dgemm over all instances */
 int irlmx_execution_plan(const irlmx_mdp* mdp, int32_t op, int64_t* plan);
 
 /*
@@ -203,6 +212,15 @@ int irlmx_dense_to_stencil(const double* dense, int32_t width, int32_t height, i
  * conversion of the reference's dense p_transition (maxent.py:98-102, 143) for
  * non-grid models.
  */
+/*
+ * Dense [S][S][A] float64 table (device, the reference's p_transition layout)
+ * -> DENSE layout: p_rows [A][S][S] (P[s, t, a] at [a][s][t]) and m_rows [S][S]
+ * (sum over actions in action order).  Replaces the per-call slice copies of
+ * maxent.py:98-102, 143, 320 and solver.py:37 for genuinely dense models.
+ */
+int irlmx_dense_to_rows(const double* dense, int32_t n_states, int32_t n_actions, double* p_rows, double* m_rows,
+                        void* stream);
+
 int irlmx_dense_ell_sizes(const double* dense, int32_t n_states, int32_t n_actions, int32_t* k_out,
                           int32_t* col_count, void* stream);
 int irlmx_dense_to_ell(const double* dense, int32_t n_states, int32_t n_actions, int32_t k_row, int32_t k_col,

@@ -52,6 +52,8 @@ __device__ inline unsigned long long abs_bits(double x) {
   return (unsigned long long)__double_as_longlong(fabs(x));
 }
 
+#define kNaN (__longlong_as_double(0x7ff8000000000000LL))
+
 __device__ inline double bits_double(unsigned long long u) {
   return __longlong_as_double((long long)u);
 }

@@ -1,0 +1,70 @@
+// Dense-row path (IRLMX_LAYOUT_DENSE): shared declarations between dense.hip
+// (kernels) and fixed_point.hip (the per-sweep drivers and the C ABI).
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "common.h"
+
+namespace irlmx {
+
+// A dense model: B instances over one table (shared) or B tables.
+struct DenseView {
+  int S, A, B, shared;
+  const double* P;  // [B'][A][S][S]: P[s, t, a] at [a][s][t]
+  const double* M;  // [B'][S][S]:    sum_a P[s, t, a]
+};
+
+// Per-sweep state, the same conventions as the sweep shape (fixed_point.hip Ws):
+// ping-pong vectors, a 3-slot ring of per-instance max|.| words, done flags.
+struct DenseBufs {
+  double* buf0;               // [B][S]
+  double* buf1;               // [B][S]
+  unsigned long long* slots;  // [B][3]
+  int32_t* done;              // [B]
+  int64_t* iters;             // [B]
+  int32_t* ndone;             // [1]
+  int32_t* bad;               // [B] non-finite policy (forward) / partition value (backward)
+  double* wt;                 // forward: [B][S][S] per-instance gather matrix WT[t][s]; GEMM: [B][S] product
+};
+
+struct DenseBellman {  // soft VI (maxent.py:326-338) / VI (solver.py:40-50)
+  const double* reward;
+  const double* phi;
+  double discount;
+  double eps;
+  long long max_iter;
+  int average;
+  int soft;
+  double* pi;
+  double* value;
+  int64_t* iters;
+  int32_t* status;
+};
+
+constexpr int kDenseMaxActions = 8;
+// rows of a dense kernel launch: 4 waves x kDenseRowsPerWave rows per workgroup
+constexpr int kDenseThreads = 256;
+constexpr int kDenseRowsPerWave = 2;
+constexpr int kDenseRowsPerBlock = (kDenseThreads / kWave) * kDenseRowsPerWave;
+constexpr int kDenseLdsMaxStates = 8192;    // the swept vector is staged in LDS up to here (64 KiB)
+
+void dense_rows_launch(const double* dense, int S, int A, double* P, double* M, hipStream_t st);
+void dense_fwd_weights_launch(const DenseView& d, const double* pi, const uint8_t* term, DenseBufs w,
+                              hipStream_t st);
+void dense_fwd_sweep_launch(const DenseView& d, const double* p0, double eps, long long max_iter, int32_t* status,
+                            DenseBufs w, long long it, int r3, hipStream_t st);
+void dense_bwd_init_launch(const DenseView& d, const uint8_t* term, DenseBufs w, hipStream_t st);
+void dense_bwd_sweep_launch(const DenseView& d, const double* reward, int rescale, DenseBufs w, long long it, int r3,
+                            hipStream_t st);
+// shared table, all B instances: the epilogue of a GEMM sweep (w.wt = M . ZS)
+void dense_bwd_gemm_epilogue_launch(const DenseView& d, const double* reward, int rescale, DenseBufs w, long long it,
+                                    int r3, hipStream_t st);
+void dense_bwd_final_launch(const DenseView& d, const double* reward, int rescale, double* pi, int32_t* status,
+                            DenseBufs w, long long collapsed, int r3, hipStream_t st);
+void dense_bellman_sweep_launch(const DenseView& d, const DenseBellman& a, DenseBufs w, long long it, int r3,
+                                hipStream_t st);
+void dense_bellman_finish_launch(const DenseView& d, const DenseBellman& a, DenseBufs w, hipStream_t st);
+
+}  // namespace irlmx

@@ -1,0 +1,468 @@
+// Dense-row kernels (IRLMX_LAYOUT_DENSE) for transition models whose rows are
+// mostly nonzero -- non-grid MDPs where the ELL layout would gather ~S slots
+// per state.  Each kernel is one sweep of a reference statement over all B
+// instances, with the swept vector staged in LDS and the matrix rows streamed
+// from HBM, one wave per output row (64 lanes x 16 B = 1 KiB per coalesced
+// load, four independent FMA chains per lane, butterfly sum):
+//
+//   backward   zs'[s] = exp(r[s]) * (M zs)[s],  M = sum_a P_a  (maxent.py:155-156)
+//   final      za[s, a] = exp(r[s]) * (P_a zs)[s]; pi = za / sum_a za (maxent.py:155-159)
+//   forward    d'[t] = p0[t] + (WT d)[t],  WT[t][s] = sum_a P'[s, t, a] pi[s, a]
+//                                                          (maxent.py:98-112)
+//   soft VI    v'[s] = fold_a softmax(v', r[s] + g (P_a v)[s]) from phi  (maxent.py:326-338)
+//   VI         v'[s] = r[s] + max_a / mean_a g (P_a v)[s]            (solver.py:40-50, 95-100)
+//
+// All are HBM-stream bound (S^2 doubles per sweep per table and instance).
+// With one table shared by B instances the backward sweep is a GEMM
+// (M . [zs_1 .. zs_B]); fixed_point.hip then runs it as a library dgemm plus the
+// epilogue below, or streams M once per instance -- whichever the planner's
+// measured crossover picks.  Convergence bookkeeping follows the
+// sweep shape of fixed_point.hip (3-slot max ring, done flags, host polling).
+
+#include <hip/hip_runtime.h>
+
+#include "dense.h"
+
+namespace irlmx {
+
+namespace {
+
+__device__ inline int dense_finish_status(double delta, double eps) {
+  if (delta != delta) return IRLMX_NONFINITE;
+  return delta > eps ? IRLMX_MAXITER : IRLMX_OK;
+}
+
+// The reference's loop test for instance b before sweep `it` (fixed_point.hip
+// sweep_should_stop): stop after the first sweep whose max|delta| is not > eps.
+__device__ inline bool dense_should_stop(int b, long long it, int r3, double eps, long long max_iter,
+                                         const DenseBufs& w, int32_t* status) {
+  if (w.done[b]) return true;
+  if (it == 0) return false;
+  const double prev = bits_double(w.slots[b * 3 + (r3 == 0 ? 2 : r3 - 1)]);
+  const bool cap = max_iter > 0 && it >= max_iter;
+  if (prev > eps && !cap) return false;
+  if (blockIdx.x == 0 && threadIdx.x == 0) {
+    w.done[b] = 1;
+    w.iters[b] = it;
+    status[b] = dense_finish_status(prev, eps);
+    atomicAdd(w.ndone, 1);
+  }
+  return true;
+}
+
+// Copy the swept vector into LDS (S <= kDenseLdsMaxStates), else read it in place.
+template <bool LDSV>
+__device__ inline const double* stage(const double* __restrict__ src, double* lds, int S) {
+  if constexpr (!LDSV) {
+    return src;
+  } else {
+    if ((S & 1) == 0) {
+      const double2* s2 = reinterpret_cast<const double2*>(src);
+      double2* l2 = reinterpret_cast<double2*>(lds);
+      for (int i = threadIdx.x; i < (S >> 1); i += blockDim.x) l2[i] = s2[i];
+    } else {
+      for (int i = threadIdx.x; i < S; i += blockDim.x) lds[i] = src[i];
+    }
+    __syncthreads();
+    return lds;
+  }
+}
+
+// Dot product of one matrix row with v, by one wave; every lane returns the
+// same sum (the butterfly adds the same pair on both partners: commutative).
+__device__ inline double wave_dot(const double* __restrict__ row, const double* __restrict__ v, int S, int lane) {
+  double a0 = 0.0, a1 = 0.0, a2 = 0.0, a3 = 0.0;
+  if ((S & 1) == 0) {
+    const double2* r2 = reinterpret_cast<const double2*>(row);
+    const double2* v2 = reinterpret_cast<const double2*>(v);
+    const int n2 = S >> 1;
+    int j = lane;
+    for (; j + 64 < n2; j += 128) {
+      const double2 x = r2[j];
+      const double2 y = r2[j + 64];
+      const double2 p = v2[j], q = v2[j + 64];
+      a0 = fma(x.x, p.x, a0);
+      a1 = fma(x.y, p.y, a1);
+      a2 = fma(y.x, q.x, a2);
+      a3 = fma(y.y, q.y, a3);
+    }
+    if (j < n2) {
+      const double2 x = r2[j];
+      const double2 p = v2[j];
+      a0 = fma(x.x, p.x, a0);
+      a1 = fma(x.y, p.y, a1);
+    }
+  } else {
+    for (int j = lane; j < S; j += 64) a0 = fma(row[j], v[j], a0);
+  }
+  double acc = (a0 + a1) + (a2 + a3);
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) acc += __shfl_xor(acc, off, kWave);
+  return acc;
+}
+
+// Block-wide max of per-wave values (every lane of a wave holds the same value),
+// one atomic per workgroup.
+__device__ inline void block_max_slot(unsigned long long v, unsigned long long* dst) {
+  __shared__ unsigned long long red[kDenseThreads / kWave];
+  const int wv = threadIdx.x / kWave;
+  if ((threadIdx.x & (kWave - 1)) == 0) red[wv] = v;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    unsigned long long m = 0;
+    for (int i = 0; i < kDenseThreads / kWave; ++i) m = red[i] > m ? red[i] : m;
+    if (m) atomicMax(dst, m);
+  }
+}
+
+__device__ inline size_t table_of(const DenseView& d, int b) { return d.shared ? 0 : (size_t)b; }
+
+}  // namespace
+
+// dense [S][S][A] -> P [A][S][S] and M [S][S] (action sum in action order)
+__global__ void dense_rows_kernel(const double* __restrict__ dense, int S, int A, double* __restrict__ P,
+                                  double* __restrict__ M) {
+  const size_t n = (size_t)S * S;
+  for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x) {
+    double acc = 0.0;
+    for (int a = 0; a < A; ++a) {
+      const double v = dense[i * A + a];
+      P[(size_t)a * n + i] = v;
+      acc += v;
+    }
+    M[i] = acc;
+  }
+}
+
+// Forward gather matrix of instance b, transposed through LDS:
+//   WT[b][t][s] = sum_a P[s, t, a] * pi[b][s][a]   (0 for terminal rows s, maxent.py:98-99)
+// so that the forward sweep reads rows of WT.  32 x 32 tiles, 256 threads.
+__global__ void __launch_bounds__(256) dense_fwd_weights_kernel(DenseView d, const double* __restrict__ pi,
+                                                                const uint8_t* __restrict__ term,
+                                                                double* __restrict__ wt) {
+  __shared__ double tile[32][33];
+  const int S = d.S, A = d.A, b = blockIdx.z;
+  const int s0 = blockIdx.y * 32, t0 = blockIdx.x * 32;
+  const int tx = threadIdx.x & 31, ty = threadIdx.x >> 5;  // 8 rows of 32
+  const double* Pb = d.P + table_of(d, b) * A * (size_t)S * S;
+  const double* pib = pi + (size_t)b * S * A;
+  for (int ii = ty; ii < 32; ii += 8) {
+    const int s = s0 + ii, t = t0 + tx;
+    double acc = 0.0;
+    if (s < S && t < S && !term[(size_t)b * S + s])
+      for (int a = 0; a < A; ++a) acc = fma(Pb[((size_t)a * S + s) * S + t], pib[(size_t)s * A + a], acc);
+    tile[ii][tx] = acc;
+  }
+  __syncthreads();
+  for (int jj = ty; jj < 32; jj += 8) {
+    const int t = t0 + jj, s = s0 + tx;
+    if (t < S && s < S) wt[((size_t)b * S + t) * S + s] = tile[tx][jj];
+  }
+}
+
+// non-finite policy entries: the reference's dense product is NaN everywhere
+// after one sweep (fixed_point.hip fwd_weights_kernel)
+__global__ void dense_pi_check_kernel(const double* __restrict__ pi, int n, int32_t* __restrict__ bad) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  const int b = blockIdx.y;
+  if (i < n && !isfinite(pi[(size_t)b * n + i])) atomicOr(&bad[b], 1);
+}
+
+template <bool LDSV>
+__global__ void __launch_bounds__(kDenseThreads)
+dense_fwd_sweep_kernel(DenseView d, const double* __restrict__ p0, double eps, long long max_iter,
+                       int32_t* __restrict__ status, DenseBufs w, long long it, int r3) {
+  extern __shared__ __attribute__((aligned(16))) double vs[];
+  const int b = blockIdx.y, S = d.S;
+  if (w.bad[b]) {
+    if (blockIdx.x == 0 && threadIdx.x == 0 && !w.done[b]) {
+      w.done[b] = 1; w.iters[b] = 1; status[b] = IRLMX_NONFINITE; atomicAdd(w.ndone, 1);
+    }
+    return;
+  }
+  if (dense_should_stop(b, it, r3, eps, max_iter, w, status)) return;
+  const double* din = ((it & 1) ? w.buf1 : w.buf0) + (size_t)b * S;
+  double* dout = ((it & 1) ? w.buf0 : w.buf1) + (size_t)b * S;
+  const double* v = stage<LDSV>(din, vs, S);
+  const int wave = threadIdx.x / kWave, lane = threadIdx.x & (kWave - 1);
+  unsigned long long mx = 0ull;
+  for (int i = 0; i < kDenseRowsPerWave; ++i) {
+    const int t = blockIdx.x * kDenseRowsPerBlock + wave * kDenseRowsPerWave + i;
+    if (t >= S) break;
+    const double acc = wave_dot(w.wt + ((size_t)b * S + t) * S, v, S, lane);
+    const double nv = p0[(size_t)b * S + t] + acc;   // maxent.py:110
+    if (lane == 0) dout[t] = nv;
+    const unsigned long long dd = abs_bits(nv - v[t]);
+    mx = dd > mx ? dd : mx;
+  }
+  block_max_slot(mx, &w.slots[b * 3 + r3]);
+  if (blockIdx.x == 0 && threadIdx.x == 0) w.slots[b * 3 + (r3 == 2 ? 0 : r3 + 1)] = 0ull;
+}
+
+__global__ void dense_bwd_init_kernel(int S, const uint8_t* __restrict__ term, double* __restrict__ buf0) {
+  const int s = blockIdx.x * blockDim.x + threadIdx.x;
+  const int b = blockIdx.y;
+  if (s < S) buf0[(size_t)b * S + s] = term[(size_t)b * S + s] ? 1.0 : 0.0;   // maxent.py:146-147
+}
+
+// One collapsed backward sweep, streaming M once per instance.
+template <bool LDSV>
+__global__ void __launch_bounds__(kDenseThreads)
+dense_bwd_sweep_kernel(DenseView d, const double* __restrict__ reward, int rescale, DenseBufs w, long long it,
+                       int r3) {
+  extern __shared__ __attribute__((aligned(16))) double vs[];
+  const int b = blockIdx.y, S = d.S;
+  const double* din = ((it & 1) ? w.buf1 : w.buf0) + (size_t)b * S;
+  double* dout = ((it & 1) ? w.buf0 : w.buf1) + (size_t)b * S;
+  int e = 0;
+  if (rescale && it > 0) e = rescale_exponent(bits_double(w.slots[b * 3 + (r3 == 0 ? 2 : r3 - 1)]));
+  const double* v = stage<LDSV>(din, vs, S);
+  const double* M = d.M + table_of(d, b) * (size_t)S * S;
+  const int wave = threadIdx.x / kWave, lane = threadIdx.x & (kWave - 1);
+  unsigned long long mx = 0ull;
+  for (int i = 0; i < kDenseRowsPerWave; ++i) {
+    const int s = blockIdx.x * kDenseRowsPerBlock + wave * kDenseRowsPerWave + i;
+    if (s >= S) break;
+    const double acc = wave_dot(M + (size_t)s * S, v, S, lane);
+    const double nv = ldexp(__dmul_rn(exp(reward[(size_t)b * S + s]), acc), e);
+    if (lane == 0) {
+      dout[s] = nv;
+      if (!isfinite(nv)) atomicOr(&w.bad[b], 1);   // fixed_point.hip bwd_nonfinite_rule
+    }
+    const unsigned long long dd = abs_bits(nv);
+    mx = dd > mx ? dd : mx;
+  }
+  if (rescale) {
+    block_max_slot(mx, &w.slots[b * 3 + r3]);
+    if (blockIdx.x == 0 && threadIdx.x == 0) w.slots[b * 3 + (r3 == 2 ? 0 : r3 + 1)] = 0ull;
+  }
+}
+
+// Epilogue of a GEMM sweep (shared table): w.wt[b][s] = (M . zs_b)[s].
+__global__ void __launch_bounds__(kDenseThreads)
+dense_bwd_gemm_epilogue_kernel(int S, const double* __restrict__ reward, int rescale, DenseBufs w, long long it,
+                               int r3) {
+  const int b = blockIdx.y;
+  const int s = blockIdx.x * blockDim.x + threadIdx.x;
+  double* dout = ((it & 1) ? w.buf0 : w.buf1) + (size_t)b * S;
+  int e = 0;
+  if (rescale && it > 0) e = rescale_exponent(bits_double(w.slots[b * 3 + (r3 == 0 ? 2 : r3 - 1)]));
+  unsigned long long mx = 0ull;
+  if (s < S) {
+    const double nv = ldexp(__dmul_rn(exp(reward[(size_t)b * S + s]), w.wt[(size_t)b * S + s]), e);
+    dout[s] = nv;
+    if (!isfinite(nv)) atomicOr(&w.bad[b], 1);
+    mx = abs_bits(nv);
+  }
+  if (rescale) {
+    for (int off = 32; off > 0; off >>= 1) {
+      const unsigned long long o = __shfl_xor(mx, off, kWave);
+      mx = o > mx ? o : mx;
+    }
+    block_max_slot(mx, &w.slots[b * 3 + r3]);
+    if (blockIdx.x == 0 && threadIdx.x == 0) w.slots[b * 3 + (r3 == 2 ? 0 : r3 + 1)] = 0ull;
+  }
+}
+
+// The last of the 2*S sweeps, per action: za = exp(r) * (P_a zs); pi = za / sum_a za.
+template <bool LDSV>
+__global__ void __launch_bounds__(kDenseThreads)
+dense_bwd_final_kernel(DenseView d, const double* __restrict__ reward, int rescale, double* __restrict__ pi,
+                       int32_t* __restrict__ status, DenseBufs w, long long collapsed, int r3) {
+  extern __shared__ __attribute__((aligned(16))) double vs[];
+  const int b = blockIdx.y, S = d.S, A = d.A;
+  const int wave = threadIdx.x / kWave, lane = threadIdx.x & (kWave - 1);
+  if (w.bad[b]) {  // bwd_nonfinite_rule
+    for (int i = 0; i < kDenseRowsPerWave; ++i) {
+      const int s = blockIdx.x * kDenseRowsPerBlock + wave * kDenseRowsPerWave + i;
+      if (s < S && lane < A) pi[((size_t)b * S + s) * A + lane] = kNaN;
+    }
+    if (blockIdx.x == 0 && threadIdx.x == 0) status[b] = IRLMX_OK;
+    return;
+  }
+  const double* zs = ((collapsed & 1) ? w.buf1 : w.buf0) + (size_t)b * S;
+  int e = 0;
+  if (rescale && collapsed > 0) e = rescale_exponent(bits_double(w.slots[b * 3 + (r3 == 0 ? 2 : r3 - 1)]));
+  const double* v = stage<LDSV>(zs, vs, S);
+  const double* Pb = d.P + table_of(d, b) * A * (size_t)S * S;
+  for (int i = 0; i < kDenseRowsPerWave; ++i) {
+    const int s = blockIdx.x * kDenseRowsPerBlock + wave * kDenseRowsPerWave + i;
+    if (s >= S) break;
+    const double er = exp(reward[(size_t)b * S + s]);
+    double za[kDenseMaxActions];
+    double zsum = 0.0;
+#pragma unroll
+    for (int act = 0; act < kDenseMaxActions; ++act) {
+      za[act] = 0.0;
+      if (act < A) {
+        const double acc = wave_dot(Pb + ((size_t)act * S + s) * S, v, S, lane);
+        za[act] = ldexp(__dmul_rn(er, acc), e);   // rounded product, then the sum (maxent.py:155-156)
+        zsum = __dadd_rn(zsum, za[act]);
+      }
+    }
+    double z = za[0];
+#pragma unroll
+    for (int act = 1; act < kDenseMaxActions; ++act) z = lane == act ? za[act] : z;
+    if (lane < A) pi[((size_t)b * S + s) * A + lane] = z / zsum;   // maxent.py:159
+  }
+  if (blockIdx.x == 0 && threadIdx.x == 0) status[b] = IRLMX_OK;
+}
+
+// Bellman backup of one state from its A action dots (fixed_point.hip bellman_update).
+__device__ inline double dense_backup(const DenseBellman& a, int A, const double (&dots)[kDenseMaxActions], double r,
+                                     double phi) {
+  double v = a.soft ? phi : 0.0;
+#pragma unroll
+  for (int act = 0; act < kDenseMaxActions; ++act) {
+    if (act >= A) break;
+    if (a.soft) {
+      v = softmax2(v, __dadd_rn(r, __dmul_rn(a.discount, dots[act])));   // maxent.py:329-333
+    } else {
+      const double q = __dmul_rn(a.discount, dots[act]);                 // solver.py:44
+      if (a.average) v = act == 0 ? q : __dadd_rn(v, q);
+      else v = act == 0 ? q : ((v != v || q <= v) ? v : q);
+    }
+  }
+  if (!a.soft) v = __dadd_rn(r, a.average ? v / (double)A : v);           // solver.py:47 / :99
+  return v;
+}
+
+template <bool LDSV>
+__global__ void __launch_bounds__(kDenseThreads)
+dense_bellman_sweep_kernel(DenseView d, DenseBellman a, DenseBufs w, long long it, int r3) {
+  extern __shared__ __attribute__((aligned(16))) double vs[];
+  const int b = blockIdx.y, S = d.S, A = d.A;
+  if (dense_should_stop(b, it, r3, a.eps, a.max_iter, w, a.status)) return;
+  const double* vin = ((it & 1) ? w.buf1 : w.buf0) + (size_t)b * S;
+  double* vout = ((it & 1) ? w.buf0 : w.buf1) + (size_t)b * S;
+  const double* v = stage<LDSV>(vin, vs, S);
+  const double* Pb = d.P + table_of(d, b) * A * (size_t)S * S;
+  const int wave = threadIdx.x / kWave, lane = threadIdx.x & (kWave - 1);
+  unsigned long long mx = 0ull;
+  for (int i = 0; i < kDenseRowsPerWave; ++i) {
+    const int s = blockIdx.x * kDenseRowsPerBlock + wave * kDenseRowsPerWave + i;
+    if (s >= S) break;
+    double dots[kDenseMaxActions];
+#pragma unroll
+    for (int act = 0; act < kDenseMaxActions; ++act)
+      dots[act] = act < A ? wave_dot(Pb + ((size_t)act * S + s) * S, v, S, lane) : 0.0;
+    const double nv = dense_backup(a, A, dots, a.reward[(size_t)b * S + s], a.soft ? a.phi[(size_t)b * S + s] : 0.0);
+    if (lane == 0) vout[s] = nv;
+    const unsigned long long dd = abs_bits(nv - v[s]);
+    mx = dd > mx ? dd : mx;
+  }
+  block_max_slot(mx, &w.slots[b * 3 + r3]);
+  if (blockIdx.x == 0 && threadIdx.x == 0) w.slots[b * 3 + (r3 == 2 ? 0 : r3 + 1)] = 0ull;
+}
+
+// value out; soft VI: pi = exp(q - v) with q from the last sweep's input (maxent.py:341)
+template <bool LDSV>
+__global__ void __launch_bounds__(kDenseThreads)
+dense_bellman_finish_kernel(DenseView d, DenseBellman a, DenseBufs w) {
+  extern __shared__ __attribute__((aligned(16))) double vs[];
+  const int b = blockIdx.y, S = d.S, A = d.A;
+  const long long it = w.iters[b];
+  const double* vnew = ((it & 1) ? w.buf1 : w.buf0) + (size_t)b * S;
+  const double* vold = ((it & 1) ? w.buf0 : w.buf1) + (size_t)b * S;
+  const double* v = stage<LDSV>(vold, vs, S);
+  const double* Pb = d.P + table_of(d, b) * A * (size_t)S * S;
+  const int wave = threadIdx.x / kWave, lane = threadIdx.x & (kWave - 1);
+  for (int i = 0; i < kDenseRowsPerWave; ++i) {
+    const int s = blockIdx.x * kDenseRowsPerBlock + wave * kDenseRowsPerWave + i;
+    if (s >= S) break;
+    const double vn = vnew[s];
+    if (lane == 0 && a.value) a.value[(size_t)b * S + s] = vn;
+    if (a.soft) {
+      const double r = a.reward[(size_t)b * S + s];
+      for (int act = 0; act < A; ++act) {
+        const double dot = wave_dot(Pb + ((size_t)act * S + s) * S, v, S, lane);
+        const double q = __dadd_rn(r, __dmul_rn(a.discount, dot));
+        if (lane == 0) a.pi[((size_t)b * S + s) * A + act] = exp(q - vn);
+      }
+    }
+  }
+  if (blockIdx.x == 0 && threadIdx.x == 0 && a.iters) a.iters[b] = it;
+}
+
+// ---------------------------------------------------------------------------
+// launchers
+// ---------------------------------------------------------------------------
+
+namespace {
+dim3 row_grid(const DenseView& d) { return dim3((d.S + kDenseRowsPerBlock - 1) / kDenseRowsPerBlock, d.B); }
+bool lds_vec(int S) { return S <= kDenseLdsMaxStates; }
+size_t lds_bytes(int S) { return lds_vec(S) ? (size_t)S * sizeof(double) : 0; }
+}  // namespace
+
+void dense_rows_launch(const double* dense, int S, int A, double* P, double* M, hipStream_t st) {
+  const size_t n = (size_t)S * S;
+  const int blocks = (int)std::min<size_t>((n + 255) / 256, 65536);
+  hipLaunchKernelGGL(dense_rows_kernel, dim3(blocks), dim3(256), 0, st, dense, S, A, P, M);
+}
+
+void dense_fwd_weights_launch(const DenseView& d, const double* pi, const uint8_t* term, DenseBufs w,
+                              hipStream_t st) {
+  const int nt = (d.S + 31) / 32;
+  hipLaunchKernelGGL(dense_fwd_weights_kernel, dim3(nt, nt, d.B), dim3(256), 0, st, d, pi, term, w.wt);
+  hipLaunchKernelGGL(dense_pi_check_kernel, dim3((d.S * d.A + 255) / 256, d.B), dim3(256), 0, st, pi, d.S * d.A,
+                     w.bad);
+}
+
+void dense_fwd_sweep_launch(const DenseView& d, const double* p0, double eps, long long max_iter, int32_t* status,
+                            DenseBufs w, long long it, int r3, hipStream_t st) {
+  if (lds_vec(d.S))
+    hipLaunchKernelGGL(dense_fwd_sweep_kernel<true>, row_grid(d), dim3(kDenseThreads), lds_bytes(d.S), st, d, p0, eps,
+                       max_iter, status, w, it, r3);
+  else
+    hipLaunchKernelGGL(dense_fwd_sweep_kernel<false>, row_grid(d), dim3(kDenseThreads), 0, st, d, p0, eps, max_iter,
+                       status, w, it, r3);
+}
+
+void dense_bwd_init_launch(const DenseView& d, const uint8_t* term, DenseBufs w, hipStream_t st) {
+  hipLaunchKernelGGL(dense_bwd_init_kernel, dim3((d.S + 255) / 256, d.B), dim3(256), 0, st, d.S, term, w.buf0);
+}
+
+void dense_bwd_sweep_launch(const DenseView& d, const double* reward, int rescale, DenseBufs w, long long it, int r3,
+                            hipStream_t st) {
+  if (lds_vec(d.S))
+    hipLaunchKernelGGL(dense_bwd_sweep_kernel<true>, row_grid(d), dim3(kDenseThreads), lds_bytes(d.S), st, d, reward,
+                       rescale, w, it, r3);
+  else
+    hipLaunchKernelGGL(dense_bwd_sweep_kernel<false>, row_grid(d), dim3(kDenseThreads), 0, st, d, reward, rescale, w,
+                       it, r3);
+}
+
+void dense_bwd_gemm_epilogue_launch(const DenseView& d, const double* reward, int rescale, DenseBufs w, long long it,
+                                    int r3, hipStream_t st) {
+  hipLaunchKernelGGL(dense_bwd_gemm_epilogue_kernel, dim3((d.S + kDenseThreads - 1) / kDenseThreads, d.B),
+                     dim3(kDenseThreads), 0, st, d.S, reward, rescale, w, it, r3);
+}
+
+void dense_bwd_final_launch(const DenseView& d, const double* reward, int rescale, double* pi, int32_t* status,
+                            DenseBufs w, long long collapsed, int r3, hipStream_t st) {
+  if (lds_vec(d.S))
+    hipLaunchKernelGGL(dense_bwd_final_kernel<true>, row_grid(d), dim3(kDenseThreads), lds_bytes(d.S), st, d, reward,
+                       rescale, pi, status, w, collapsed, r3);
+  else
+    hipLaunchKernelGGL(dense_bwd_final_kernel<false>, row_grid(d), dim3(kDenseThreads), 0, st, d, reward, rescale,
+                       pi, status, w, collapsed, r3);
+}
+
+void dense_bellman_sweep_launch(const DenseView& d, const DenseBellman& a, DenseBufs w, long long it, int r3,
+                                hipStream_t st) {
+  if (lds_vec(d.S))
+    hipLaunchKernelGGL(dense_bellman_sweep_kernel<true>, row_grid(d), dim3(kDenseThreads), lds_bytes(d.S), st, d, a,
+                       w, it, r3);
+  else
+    hipLaunchKernelGGL(dense_bellman_sweep_kernel<false>, row_grid(d), dim3(kDenseThreads), 0, st, d, a, w, it, r3);
+}
+
+void dense_bellman_finish_launch(const DenseView& d, const DenseBellman& a, DenseBufs w, hipStream_t st) {
+  if (lds_vec(d.S))
+    hipLaunchKernelGGL(dense_bellman_finish_kernel<true>, row_grid(d), dim3(kDenseThreads), lds_bytes(d.S), st, d, a,
+                       w);
+  else
+    hipLaunchKernelGGL(dense_bellman_finish_kernel<false>, row_grid(d), dim3(kDenseThreads), 0, st, d, a, w);
+}
+
+}  // namespace irlmx

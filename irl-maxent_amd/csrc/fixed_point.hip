@@ -32,8 +32,11 @@
 #include <cstring>
 #include <vector>
 
+#include <rocblas/rocblas.h>
+
 #include "cluster.h"
 #include "common.h"
+#include "dense.h"
 
 namespace irlmx {
 
@@ -63,7 +66,7 @@ constexpr int kSweepThreads = 256;
 // ---------------------------------------------------------------------------
 
 struct Model {
-  int S, A, K, W, H, B, stencil, shared, Kc;
+  int S, A, K, W, H, B, stencil, shared, Kc, dense;
   const double* row_val;
   const int32_t* row_idx;
   const int32_t* col_idx;
@@ -75,8 +78,9 @@ static Model make_model(const irlmx_mdp* m) {
   o.S = m->n_states;
   o.A = m->n_actions;
   o.stencil = m->layout == IRLMX_LAYOUT_STENCIL5;
-  o.K = o.stencil ? kStencilK : m->k_row;
-  o.Kc = o.stencil ? kStencilK : m->k_col;
+  o.dense = m->layout == IRLMX_LAYOUT_DENSE;
+  o.K = o.stencil ? kStencilK : (o.dense ? m->n_states : m->k_row);
+  o.Kc = o.stencil ? kStencilK : (o.dense ? m->n_states : m->k_col);
   o.W = m->width;
   o.H = m->height;
   o.B = m->batch;
@@ -142,8 +146,8 @@ static Ws carve(const Model& m, int op, void* base) {
   };
   const size_t B = m.B, S = m.S;
   size_t nw = 0;
-  if (op == IRLMX_OP_FORWARD) nw = B * m.Kc * S;
-  if (op == IRLMX_OP_BACKWARD) nw = B * m.K * S;  // reward-folded: one set per instance
+  if (op == IRLMX_OP_FORWARD) nw = B * m.Kc * S;  // dense: the per-instance gather matrices WT [B][S][S]
+  if (op == IRLMX_OP_BACKWARD) nw = m.dense ? B * S : B * m.K * S;  // reward-folded; dense: the GEMM product
   w.wgt = (double*)take(nw * sizeof(double));
   w.bad = (int32_t*)take(B * sizeof(int32_t));
   const bool sweep = !use_fused(m, op);
@@ -205,24 +209,49 @@ __global__ void fwd_weights_kernel(Model m, const double* __restrict__ pi,
   if (nonfinite) atomicOr(&bad[b], 1);
 }
 
+// bwd_nonfinite_rule.  The reference's backward product is dense (maxent.py:155:
+// P_a.dot(zs) over all S columns), so one non-finite partition value makes
+// 0 * inf = NaN appear in every row within a sweep, and the returned policy is
+// NaN everywhere.  The compact products here touch only stored neighbours, so
+// every shape records "some zs value of the 2S - 1 collapsed sweeps was
+// non-finite" (fused and sweep shapes: per sweep) and then writes NaN for the
+// whole instance.  With rescaling on, values turn non-finite only through
+// non-finite weights (a reward of +inf or NaN), which bwd_weights_kernel flags
+// (the cluster shape fills such instances with NaN after its sweeps,
+// bwd_nan_fill_kernel); calls without rescaling (the reference's overflow) do
+// not run on the cluster shape.
 // Collapsed, reward-folded backward weights of instance b:
 //   w[b][k][s] = exp(r[b][s]) * sum_a P[s, target_k(s), a]
 // so one backward sweep is zs'[s] = sum_k w[b][k][s] * zs[target_k(s)]
 // (maxent.py:155-156 with the action sum and exp(r) taken out of the loop).
 // Every shape (fused, sweep, cluster) uses these same weights in the same
 // order, so the shapes stay bit-identical to each other.
-__global__ void bwd_weights_kernel(Model m, const double* __restrict__ reward, double* __restrict__ w) {
+__global__ void bwd_weights_kernel(Model m, const double* __restrict__ reward, double* __restrict__ w,
+                                   int32_t* __restrict__ bad) {
   const int s = blockIdx.x * blockDim.x + threadIdx.x;
   const int b = blockIdx.y;
   if (s >= m.S) return;
   const size_t bi = m.shared ? 0 : (size_t)b;  // table instance
   const double er = exp(reward[(size_t)b * m.S + s]);
+  bool nf = false;
   for (int k = 0; k < m.K; ++k) {
     double acc = 0.0;
     for (int a = 0; a < m.A; ++a)
       acc += m.row_val[((bi * m.A + a) * m.K + k) * m.S + s];
-    w[((size_t)b * m.K + k) * m.S + s] = __dmul_rn(er, acc);
+    const double wk = __dmul_rn(er, acc);
+    nf |= !isfinite(wk);
+    w[((size_t)b * m.K + k) * m.S + s] = wk;
   }
+  // non-finite weights make some partition value non-finite within two sweeps,
+  // and the reference's dense product then NaN everywhere (bwd_nonfinite_rule)
+  if (nf) atomicOr(&bad[b], 1);
+}
+
+// bwd_nonfinite_rule for the cluster shape: NaN policy for flagged instances
+__global__ void bwd_nan_fill_kernel(Model m, const int32_t* __restrict__ bad, double* __restrict__ pi) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  const int b = blockIdx.y;
+  if (i < m.S * m.A && bad[b]) pi[(size_t)b * m.S * m.A + i] = kNaN;
 }
 
 // ---------------------------------------------------------------------------
@@ -367,6 +396,7 @@ __global__ void __launch_bounds__(1024) bwd_fused_kernel(BwdArgs a) {
   // table, the last one per action because it also produces za.
   const long long collapsed = 2LL * S - 1;
   int e = 0, r3 = 0;
+  bool nf = false;  // some partition value went non-finite (see bwd_nonfinite_rule)
   for (long long it = 0; it < collapsed; ++it) {
     const double* din = (it & 1) ? bufB : bufA;
     double* dout = (it & 1) ? bufA : bufB;
@@ -384,6 +414,7 @@ __global__ void __launch_bounds__(1024) bwd_fused_kernel(BwdArgs a) {
         dout[s] = nv;
         const unsigned long long d = abs_bits(nv);
         mx = d > mx ? d : mx;
+        nf |= !isfinite(nv);
       }
     }
     if (a.rescale) {
@@ -396,10 +427,13 @@ __global__ void __launch_bounds__(1024) bwd_fused_kernel(BwdArgs a) {
   }
   const double* zs = (collapsed & 1) ? bufB : bufA;
   if (a.rescale && collapsed > 0) e = rescale_exponent(bits_double(slot[r3 == 0 ? 2 : r3 - 1]));
+  const bool all_nan = __syncthreads_or(nf);
 #pragma unroll
   for (int j = 0; j < SPT; ++j) {
     const int s = tid + j * nt;
-    if (s < S) {
+    if (s < S && all_nan) {
+      for (int act = 0; act < A; ++act) a.pi[((size_t)b * S + s) * A + act] = kNaN;
+    } else if (s < S) {
       const double er = exp(a.reward[(size_t)b * S + s]);
       double za[kMaxActions];
       double zsum = 0.0;
@@ -660,6 +694,7 @@ bwd_sweep_kernel(BwdArgs a, Ws ws, long long it, int r3) {
     const double nv = ldexp(acc, e);
     dout[s] = nv;
     d = abs_bits(nv);
+    if (!isfinite(nv)) atomicOr(&ws.bad[b], 1);  // bwd_nonfinite_rule
   }
   if (a.rescale) {
     block_max_to(d, &ws.slots[b * 3 + r3]);
@@ -680,6 +715,11 @@ __global__ void bwd_final_kernel(BwdArgs a, Ws ws, long long collapsed, int r3) 
   const int b = blockIdx.y;
   const int s = blockIdx.x * blockDim.x + threadIdx.x;
   if (s >= S) return;
+  if (ws.bad[b]) {  // bwd_nonfinite_rule
+    for (int act = 0; act < A; ++act) a.pi[((size_t)b * S + s) * A + act] = kNaN;
+    if (s == 0) a.status[b] = IRLMX_OK;
+    return;
+  }
   const double* zs = ((collapsed & 1) ? ws.buf1 : ws.buf0) + (size_t)b * S;
   int e = 0;
   if (a.rescale && collapsed > 0) e = rescale_exponent(bits_double(ws.slots[b * 3 + (r3 == 0 ? 2 : r3 - 1)]));
@@ -775,7 +815,7 @@ static constexpr bool fused_pair_ok(int op, int spt, int kmax) {
 }
 
 static bool fused_shape(const Model& m, int op, FusedShape* out) {
-  if (m.S > fused_max_states() || m.A > kMaxActions) return false;
+  if (m.dense || m.S > fused_max_states() || m.A > kMaxActions) return false;
   // Grids of width 64 / 128 run the forward and backward passes on the cluster
   // shape even when they fit one CU: its register-resident pair layouts sweep
   // 4-5x faster than the general-sparsity fused kernel, and a single instance
@@ -848,6 +888,9 @@ static int validate(const irlmx_mdp* mdp) {
     if ((long long)m.W * m.H != m.S) { set_error("stencil grid %dx%d != %d states", m.W, m.H, m.S); return IRLMX_EINVAL; }
   } else if (mdp->layout == IRLMX_LAYOUT_ELL) {
     if (!m.row_idx || m.K <= 0) { set_error("ELL row form missing"); return IRLMX_EINVAL; }
+  } else if (m.dense) {
+    if (!m.col_val) { set_error("DENSE action-summed rows (col_val) missing"); return IRLMX_EINVAL; }
+    if ((long long)m.S * m.S * m.A > (1LL << 40)) { set_error("DENSE table too large (S=%d)", m.S); return IRLMX_EINVAL; }
   } else {
     set_error("unknown layout %d", mdp->layout);
     return IRLMX_EINVAL;
@@ -889,9 +932,92 @@ static int run_until_done(const Ws& ws, int B, hipStream_t st, LaunchOne&& one) 
   }
 }
 
+// ---------------------------------------------------------------------------
+// dense-row path (dense.hip)
+// ---------------------------------------------------------------------------
+
+static DenseView dense_view(const Model& m) { return DenseView{m.S, m.A, m.B, m.shared, m.row_val, m.col_val}; }
+
+static DenseBufs dense_bufs(const Ws& ws) {
+  return DenseBufs{ws.buf0, ws.buf1, ws.slots, ws.done, ws.iters, ws.ndone, ws.bad, ws.wgt};
+}
+
+// Shared table, B instances: the collapsed backward sweep is the GEMM
+// M [S x S] . ZS [S x B].  From IRLMX_DENSE_GEMM_MIN instances on (default
+// kDenseGemmMin, measured: DESIGN.md) it runs as one library dgemm (fp64 MFMA)
+// plus an epilogue instead of streaming M once per instance on the VALU.
+constexpr int kDenseGemmMin = 4;
+static bool dense_gemm(const Model& m) {
+  return m.dense && m.shared && m.B >= getenv_int("IRLMX_DENSE_GEMM_MIN", kDenseGemmMin);
+}
+
+// one rocBLAS handle per host thread and device (handles are not thread safe)
+static int rocblas_for(hipStream_t st, rocblas_handle* out) {
+  struct Handles {
+    rocblas_handle h[64] = {};
+    ~Handles() {
+      for (auto& x : h)
+        if (x) rocblas_destroy_handle(x);
+    }
+  };
+  static thread_local Handles handles;
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) { set_error("rocblas: bad device"); return IRLMX_EHIP; }
+  if (!handles.h[dev] && rocblas_create_handle(&handles.h[dev]) != rocblas_status_success) {
+    set_error("rocblas_create_handle failed");
+    return IRLMX_EHIP;
+  }
+  if (rocblas_set_stream(handles.h[dev], st) != rocblas_status_success) { set_error("rocblas_set_stream failed"); return IRLMX_EHIP; }
+  *out = handles.h[dev];
+  return 0;
+}
+
+static int dense_backward(const Model& m, const double* reward, const uint8_t* terminal, int rescale,
+                          double* p_action, int32_t* status, const Ws& ws, hipStream_t st) {
+  const DenseView d = dense_view(m);
+  const DenseBufs w = dense_bufs(ws);
+  dense_bwd_init_launch(d, terminal, w, st);
+  const long long collapsed = 2LL * m.S - 1;
+  const bool gemm = dense_gemm(m);
+  rocblas_handle h = nullptr;
+  if (gemm)
+    if (int rc = rocblas_for(st, &h)) return rc;
+  const double one = 1.0, zero = 0.0;
+  int r3 = 0;
+  for (long long it = 0; it < collapsed; ++it) {
+    if (gemm) {
+      // column-major view: C [S x B] = op(M) . ZS with M row-major = (M^T col-major), op = transpose
+      const double* zin = (it & 1) ? ws.buf1 : ws.buf0;
+      if (rocblas_dgemm(h, rocblas_operation_transpose, rocblas_operation_none, m.S, m.B, m.S, &one, m.col_val, m.S,
+                        zin, m.S, &zero, ws.wgt, m.S) != rocblas_status_success) {
+        set_error("rocblas_dgemm failed");
+        return IRLMX_EHIP;
+      }
+      dense_bwd_gemm_epilogue_launch(d, reward, rescale, w, it, r3, st);
+    } else {
+      dense_bwd_sweep_launch(d, reward, rescale, w, it, r3, st);
+    }
+    r3 = r3 == 2 ? 0 : r3 + 1;
+  }
+  dense_bwd_final_launch(d, reward, rescale, p_action, status, w, collapsed, r3, st);
+  hipError_t e = hipGetLastError();
+  return e == hipSuccess ? 0 : hip_fail(e, "dense backward");
+}
+
 }  // namespace irlmx
 
 using namespace irlmx;
+
+extern "C" int irlmx_dense_to_rows(const double* dense, int32_t n_states, int32_t n_actions, double* p_rows,
+                                   double* m_rows, void* stream) {
+  if (!dense || !p_rows || !m_rows || n_states <= 0 || n_actions <= 0 || n_actions > kMaxActions) {
+    set_error("dense_to_rows: bad arguments");
+    return IRLMX_EINVAL;
+  }
+  dense_rows_launch(dense, n_states, n_actions, p_rows, m_rows, (hipStream_t)stream);
+  hipError_t e = hipGetLastError();
+  return e == hipSuccess ? 0 : hip_fail(e, "dense_to_rows");
+}
 
 extern "C" size_t irlmx_workspace_bytes(const irlmx_mdp* mdp, int32_t op) {
   if (validate(mdp)) return 0;
@@ -922,6 +1048,12 @@ extern "C" int irlmx_execution_plan(const irlmx_mdp* mdp, int32_t op, int64_t* p
     plan[9] = (int64_t)cp.lds;
     return 0;
   }
+  if (m.dense) {
+    plan[0] = (op == IRLMX_OP_BACKWARD && dense_gemm(m)) ? IRLMX_SHAPE_DENSE_GEMM : IRLMX_SHAPE_DENSE;
+    plan[7] = kDenseThreads;
+    plan[9] = m.S <= kDenseLdsMaxStates ? (int64_t)m.S * 8 : 0;
+    return 0;
+  }
   plan[0] = IRLMX_SHAPE_SWEEP;
   plan[7] = kSweepThreads;
   return 0;
@@ -933,19 +1065,31 @@ extern "C" int irlmx_forward_svf(const irlmx_mdp* mdp, const double* p_initial, 
                                  size_t workspace_bytes, void* stream) {
   if (int rc = validate(mdp)) return rc;
   const Model m = make_model(mdp);
-  if (!m.stencil && (!m.col_idx || !m.col_val || m.Kc <= 0)) { set_error("ELL column form missing"); return IRLMX_EINVAL; }
+  if (!m.stencil && !m.dense && (!m.col_idx || !m.col_val || m.Kc <= 0)) { set_error("ELL column form missing"); return IRLMX_EINVAL; }
   if (int rc = check_ws(m, IRLMX_OP_FORWARD, workspace_bytes, workspace)) return rc;
   hipStream_t st = (hipStream_t)stream;
   Ws ws = carve(m, IRLMX_OP_FORWARD, workspace);
   hipError_t e = hipMemsetAsync(workspace, 0, ws.total, st);
   if (e != hipSuccess) return hip_fail(e, "workspace memset");
   const dim3 g((m.S + 255) / 256, m.B);
-  hipLaunchKernelGGL(fwd_weights_kernel, g, dim3(256), 0, st, m, p_action, terminal, ws.wgt, ws.bad);
+  if (!m.dense) hipLaunchKernelGGL(fwd_weights_kernel, g, dim3(256), 0, st, m, p_action, terminal, ws.wgt, ws.bad);
   FwdArgs a{m, ws.wgt, ws.bad, p_initial, eps, (long long)max_iter, svf, iterations, status};
   FusedShape fs;
   if (fused_shape(m, IRLMX_OP_FORWARD, &fs)) {
     IRLMX_DISPATCH_FUSED(fwd_fused_ptr, fs, m.B, fused_lds(m), st, a);
     return 0;
+  }
+  if (m.dense) {  // dense rows (dense.hip): per-instance gather matrices WT, one launch per sweep
+    const DenseView d = dense_view(m);
+    const DenseBufs w = dense_bufs(ws);
+    dense_fwd_weights_launch(d, p_action, terminal, w, st);
+    int rc = run_until_done(ws, m.B, st, [&](long long it, int r3) {
+      dense_fwd_sweep_launch(d, p_initial, eps, (long long)max_iter, status, w, it, r3, st);
+    });
+    if (rc) return rc;
+    hipLaunchKernelGGL(fwd_finish_kernel, g, dim3(256), 0, st, a, ws);
+    e = hipGetLastError();
+    return e == hipSuccess ? 0 : hip_fail(e, "dense forward");
   }
   ClusterPlan cp;
   if (m.stencil && cluster_plan(m.W, m.H, m.B, kModeFwd, &cp)) {
@@ -984,7 +1128,8 @@ extern "C" int irlmx_backward_maxent(const irlmx_mdp* mdp, const double* reward,
   Ws ws = carve(m, IRLMX_OP_BACKWARD, workspace);
   hipError_t e = hipMemsetAsync(workspace, 0, ws.total, st);
   if (e != hipSuccess) return hip_fail(e, "workspace memset");
-  hipLaunchKernelGGL(bwd_weights_kernel, dim3((m.S + 255) / 256, m.B), dim3(256), 0, st, m, reward, ws.wgt);
+  if (m.dense) return dense_backward(m, reward, terminal, rescale, p_action, status, ws, st);
+  hipLaunchKernelGGL(bwd_weights_kernel, dim3((m.S + 255) / 256, m.B), dim3(256), 0, st, m, reward, ws.wgt, ws.bad);
   BwdArgs a{m, ws.wgt, reward, terminal, rescale, p_action, status};
   FusedShape fs;
   if (fused_shape(m, IRLMX_OP_BACKWARD, &fs)) {
@@ -992,7 +1137,9 @@ extern "C" int irlmx_backward_maxent(const irlmx_mdp* mdp, const double* reward,
     return 0;
   }
   ClusterPlan cp;
-  if (m.stencil && m.A <= kMaxActions && cluster_plan(m.W, m.H, m.B, kModeBwd, &cp)) {
+  // (without rescaling the partition vector overflows like the reference's: such
+  // calls take the per-sweep shape, whose non-finite bookkeeping is per sweep)
+  if (m.stencil && m.A <= kMaxActions && rescale && cluster_plan(m.W, m.H, m.B, kModeBwd, &cp)) {
     hipLaunchKernelGGL(bwd_growth_kernel, dim3(m.B), dim3(1024), 0, st, ws.wgt, m.S, ws.growth);
     ClusterArgs ca{};
     ca.W = m.W; ca.H = m.H; ca.S = m.S; ca.A = m.A;
@@ -1001,7 +1148,12 @@ extern "C" int irlmx_backward_maxent(const irlmx_mdp* mdp, const double* reward,
     ca.n_sweeps = 2LL * m.S - 1; ca.rescale = rescale;
     ca.gran = ws.gran; ca.sgran = ws.sgran; ca.err = ws.err;
     ca.out = p_action; ca.status = status;
-    return cluster_run(kModeBwd, cp, ca, m.B, st);
+    if (int rc = cluster_run(kModeBwd, cp, ca, m.B, st)) return rc;
+    // instances with non-finite weights: all NaN (bwd_nonfinite_rule), outside the sweep kernel
+    hipLaunchKernelGGL(bwd_nan_fill_kernel, dim3((m.S * m.A + 255) / 256, m.B), dim3(256), 0, st, m, ws.bad,
+                       p_action);
+    e = hipGetLastError();
+    return e == hipSuccess ? 0 : hip_fail(e, "backward nan fill");
   }
   const dim3 g((m.S + kSweepThreads - 1) / kSweepThreads, m.B);
   hipLaunchKernelGGL(bwd_init_kernel, g, dim3(kSweepThreads), 0, st, a, ws);
@@ -1038,6 +1190,17 @@ static int bellman_common(const irlmx_mdp* mdp, const double* reward, const doub
   const dim3 g((m.S + kSweepThreads - 1) / kSweepThreads, m.B);
   const size_t n = (size_t)m.B * m.S;
   hipLaunchKernelGGL(fill_kernel, dim3((n + 255) / 256), dim3(256), 0, st, ws.buf0, n, soft ? -1e200 : 0.0);
+  if (m.dense) {  // dense rows (dense.hip)
+    const DenseView d = dense_view(m);
+    const DenseBufs w = dense_bufs(ws);
+    const DenseBellman db{reward, phi, discount, eps, (long long)max_iter, average, soft ? 1 : 0, p_action, value,
+                          iterations, status};
+    int rc = run_until_done(ws, m.B, st, [&](long long it, int r3) { dense_bellman_sweep_launch(d, db, w, it, r3, st); });
+    if (rc) return rc;
+    dense_bellman_finish_launch(d, db, w, st);
+    e = hipGetLastError();
+    return e == hipSuccess ? 0 : hip_fail(e, "dense bellman");
+  }
   int rc = run_until_done(ws, m.B, st, [&](long long it, int r3) {
     if (soft) hipLaunchKernelGGL(bellman_sweep_kernel<true>, g, dim3(kSweepThreads), 0, st, a, ws, it, r3);
     else hipLaunchKernelGGL(bellman_sweep_kernel<false>, g, dim3(kSweepThreads), 0, st, a, ws, it, r3);

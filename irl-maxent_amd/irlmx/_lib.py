@@ -19,6 +19,7 @@ LIB_PATH = os.environ.get("IRLMX_LIB", os.path.join(_HERE, "libirlmx.so"))
 
 LAYOUT_STENCIL5 = 1
 LAYOUT_ELL = 2
+LAYOUT_DENSE = 3
 
 SUCCESS = 0
 OK, NONFINITE, MAXITER = 0, 1, 2
@@ -72,6 +73,7 @@ SIGNATURES = {
     "irlmx_build_icy_gridworld": (ctypes.c_int, [_I32, _P, _I32, _P, _P]),
     "irlmx_build_gridworld": (ctypes.c_int, [_I32, _I32, _P, _P]),
     "irlmx_dense_to_stencil": (ctypes.c_int, [_P, _I32, _I32, _I32, _P, _P, _P]),
+    "irlmx_dense_to_rows": (ctypes.c_int, [_P, _I32, _I32, _P, _P, _P]),
     "irlmx_dense_ell_sizes": (ctypes.c_int, [_P, _I32, _I32, _P, _P, _P]),
     "irlmx_dense_to_ell": (ctypes.c_int, [_P, _I32, _I32, _I32, _I32, _P, _P, _P, _P, _P]),
 }
@@ -93,7 +95,10 @@ def load():
         _load_error = (f"irlmx: cannot load {LIB_PATH} ({e}); build it with "
                        f"`python -c 'import __graft_entry__ as g; g.build()'`")
         raise ImportError(_load_error) from e
+    variant = "IRLMX_LIB" in os.environ   # a diagnostic build may predate newer entry points
     for name, (res, args) in SIGNATURES.items():
+        if variant and not hasattr(lib, name):
+            continue
         fn = getattr(lib, name)
         fn.restype = res
         fn.argtypes = args

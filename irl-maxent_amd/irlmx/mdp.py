@@ -11,6 +11,10 @@ action]`` (gridworld.py:124-142) and re-slices it per call (maxent.py:98-102,
 * ``ELL`` -- any other sparsity: per state the union of targets over actions
   (row form, ``row_idx``/``row_val``) and, for the forward pass, the union of
   sources (column form, ``col_idx``/``col_val``).
+* ``DENSE`` -- rows mostly nonzero (ELL would gather ~S slots per state): the
+  per-action matrices ``row_val[b][a][s][t] = P[s, t, a]`` (the reference's
+  slices ``P[:, :, a]``) and their action sum ``col_val[b][s][t]``, streamed
+  row by row (dense.hip).
 
 Instances: a model holds B tables, or one table shared by B instances
 (``shared=True``), e.g. one world with B reward vectors.
@@ -79,12 +83,18 @@ class DeviceMDP:
                    "build_gridworld")
         return cls(_lib.LAYOUT_STENCIL5, S, 4, batch, False, row_val, width=size, height=size, device=device)
 
+    #: ELL slots per state above which (and above S / 8) a table is kept DENSE
+    DENSE_MIN_SLOTS = 32
+
     @classmethod
-    def from_dense(cls, p_transition, device=None, grid=None):
+    def from_dense(cls, p_transition, device=None, grid=None, layout=None):
         """Upload a dense ``[S, S, A]`` table (one instance, shared layout).
 
         The STENCIL5 layout is used when every nonzero lies on the stencil of a
-        square (or ``grid=(width, height)``) grid; otherwise ELL.
+        square (or ``grid=(width, height)``) grid; otherwise ELL, or DENSE when
+        rows are so full that ELL would gather more than ``DENSE_MIN_SLOTS`` and
+        more than S / 8 slots per state.  ``layout`` ("stencil", "ell", "dense")
+        forces one (tests; "stencil" still falls back when the table is not a grid).
         """
         device = _lib.require_device(device)
         lib = _lib.load()
@@ -98,14 +108,26 @@ class DeviceMDP:
         else:
             w = h = _is_square(S)
         dense = torch.from_numpy(p).to(device)
-        if w and w * h == S:
+        if layout == "dense":
+            return cls._dense_rows(dense, S, A, device)
+        if w and w * h == S and layout != "ell":
             row_val = torch.empty((1, A, 5, S), dtype=torch.float64, device=device)
             flag = torch.zeros(1, dtype=torch.int32, device=device)
             _lib.check(lib.irlmx_dense_to_stencil(_lib.ptr(dense), w, h, A, _lib.ptr(row_val), _lib.ptr(flag),
                                                   _lib.stream_ptr(device)), "dense_to_stencil")
             if not int(flag.item()):
                 return cls(_lib.LAYOUT_STENCIL5, S, A, 1, True, row_val, width=w, height=h, device=device)
-        return cls._ell_from_dense(dense, S, A, device)
+        return cls._ell_from_dense(dense, S, A, device, allow_dense=layout != "ell")
+
+    @classmethod
+    def _dense_rows(cls, dense, S, A, device):
+        """DENSE layout of a dense device table (irlmx_dense_to_rows)."""
+        lib = _lib.load()
+        row_val = torch.empty((1, A, S, S), dtype=torch.float64, device=device)
+        col_val = torch.empty((1, S, S), dtype=torch.float64, device=device)
+        _lib.check(lib.irlmx_dense_to_rows(_lib.ptr(dense), S, A, _lib.ptr(row_val), _lib.ptr(col_val),
+                                           _lib.stream_ptr(device)), "dense_to_rows")
+        return cls(_lib.LAYOUT_DENSE, S, A, 1, True, row_val, col_val=col_val, k_row=S, k_col=S, device=device)
 
     @classmethod
     def resident(cls, p_transition, device=None):
@@ -127,6 +149,8 @@ class DeviceMDP:
         if hit is not None and hit.device == device and hit.matches(p):
             return hit.mdp
         mdp = cls.from_dense(p, device=device)
+        if mdp.layout == _lib.LAYOUT_DENSE:
+            return mdp   # not kept: validating reuse would re-read every entry (the upload's own cost)
         while len(_RESIDENT) >= _RESIDENT_MAX:
             _RESIDENT.pop(next(iter(_RESIDENT)))
         key = id(p)
@@ -135,8 +159,9 @@ class DeviceMDP:
         return mdp
 
     @classmethod
-    def _ell_from_dense(cls, dense, S, A, device):
-        """ELL row / column forms of a dense device table (irlmx_dense_to_ell)."""
+    def _ell_from_dense(cls, dense, S, A, device, allow_dense=True):
+        """ELL row / column forms of a dense device table (irlmx_dense_to_ell), or
+        the DENSE layout when the rows are too full for ELL to pay."""
         lib = _lib.load()
         st = _lib.stream_ptr(device)
         k = torch.empty(2, dtype=torch.int32, device=device)
@@ -144,6 +169,8 @@ class DeviceMDP:
         _lib.check(lib.irlmx_dense_ell_sizes(_lib.ptr(dense), S, A, _lib.ptr(k), _lib.ptr(scratch), st),
                    "dense_ell_sizes")
         k_row, k_col = (max(1, int(v)) for v in k.tolist())
+        if allow_dense and max(k_row, k_col) > cls.DENSE_MIN_SLOTS and 8 * max(k_row, k_col) > S:
+            return cls._dense_rows(dense, S, A, device)
         row_idx = torch.empty((1, k_row, S), dtype=torch.int32, device=device)
         row_val = torch.empty((1, A, k_row, S), dtype=torch.float64, device=device)
         col_idx = torch.empty((1, k_col, S), dtype=torch.int32, device=device)
@@ -181,8 +208,8 @@ class DeviceMDP:
             s.n_actions = self.n_actions
             s.width = self.width
             s.height = self.height
-            s.k_row = self.k_row if self.layout == _lib.LAYOUT_ELL else 5
-            s.k_col = self.k_col if self.layout == _lib.LAYOUT_ELL else 5
+            s.k_row = self.k_row if self.layout != _lib.LAYOUT_STENCIL5 else 5
+            s.k_col = self.k_col if self.layout != _lib.LAYOUT_STENCIL5 else 5
             s.batch = self.batch
             s.shared = 1 if self.shared else 0
             s.row_val = self.row_val.data_ptr()
@@ -210,8 +237,10 @@ class DeviceMDP:
     def to_dense(self, b=0):
         """Dense ``[S, S, A]`` numpy table of instance b (tests and small sizes only)."""
         S, A = self.n_states, self.n_actions
-        out = np.zeros((S, S, A))
         rv = self.row_val[0 if self.shared else b].cpu().numpy()
+        if self.layout == _lib.LAYOUT_DENSE:
+            return np.ascontiguousarray(np.transpose(rv, (1, 2, 0)))
+        out = np.zeros((S, S, A))
         if self.layout == _lib.LAYOUT_STENCIL5:
             s = np.arange(S)
             x, y = s % self.width, s // self.width

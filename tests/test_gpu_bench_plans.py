@@ -86,7 +86,8 @@ def run_bench_workload(dev, cfg, size, per_gpu, n_steps, causal=False):
     assert np.array_equal(ef_dev, z[f"{b}__e_f"]) and np.array_equal(p0_dev, z[f"{b}__p0"])
     irl = BatchedMaxEnt(mdp, e_f, p0, [S - 1], causal=causal, discount=0.7 if causal else None)
     steps = []
-    for _ in range(n_steps):
+    for i in range(n_steps):
+        print(f"[{cfg}] step {i}", flush=True)
         pi = irl.backward()
         svf, iters, status = irl.forward(pi)
         irl.update(svf)
@@ -114,7 +115,13 @@ def compare_steps(z, checked, steps, n_states, causal=False):
                     assert np.all(np.abs(got - ref) <= RTOL * np.abs(ref)), (b, "pi0 sums", got, ref)
                 else:
                     close(pi, z[key + "pi0"], (b, "pi0"))
-                    assert np.argmax(pi, axis=1).tolist() == np.argmax(z[key + "pi0"], axis=1).tolist()
+                    # argmax identical wherever the best action is not tied to 1e-9
+                    # (theta0 = 1 makes mirror-symmetric states exact ties)
+                    ref = z[key + "pi0"]
+                    top = np.sort(ref, axis=1)
+                    clear = top[:, -1] - top[:, -2] > 1e-9 * np.max(ref)
+                    bad = int(np.count_nonzero(np.argmax(pi, axis=1)[clear] != np.argmax(ref, axis=1)[clear]))
+                    assert bad == 0, (b, "argmax differs at", bad, "untied states")
             for name in ("svf", "theta"):
                 vec = st[name][j]
                 ref = z[f"{key}{name}{i}"]

@@ -22,7 +22,14 @@ irlmx.demos.sample with seed 1234 + b):
                the first 2 irl_causal steps (maxent.py:437-450) of the bench's
                c5 workload (one instance, discount 0.7).
 
-Usage: python tools/gen_full_fixtures.py [c3 c4 c5]   (~15 min on 8 cores)
+  dense2048.npz  a seeded random dense MDP (S = 2048, A = 4, every entry
+               nonzero; oracle random_dense_mdp() regenerates it bit for bit on any
+               host), run through the dense oracle (the reference's own numpy
+               statements, maxent.py:98-159, 279-341; solver.py:9-104):
+               backward, forward, soft VI + causal forward, VI and its
+               action-average form, with sweep counts.
+
+Usage: python tools/gen_full_fixtures.py [c3 c4 c5 dense]   (~25 min on 8 cores)
 """
 
 import os
@@ -92,6 +99,23 @@ def job_irl(args):
     return cfg, b, out
 
 
+def job_dense(_):
+    t0 = time.time()
+    os.environ["OPENBLAS_NUM_THREADS"] = "4"
+    P, r, term, p0 = O.random_dense_mdp()
+    out = {"P_check": np.array([P.sum(), P[::7, ::5, :].sum(), P[-1, -1, -1]]), "reward": r}
+    pi = O.backward_maxent(P, term, r, rescale=True)
+    svf, k_f = O.forward_svf(P, p0, term, pi)
+    cpi, cv, k_s = O.soft_backward(P, term, r, 0.7)
+    csvf, k_cf = O.forward_svf(P, p0, term, cpi)
+    v, k_v = O.value_iteration(P, r, 0.9)
+    va, k_va = O.value_iteration(P, r, 0.9, average=True)
+    out.update(pi=pi, svf=svf, k_f=np.array(k_f), cpi=cpi, cv=cv, k_s=np.array(k_s), csvf=csvf, k_cf=np.array(k_cf),
+               v=v, k_v=np.array(k_v), va=va, k_va=np.array(k_va))
+    print(f"[dense] k_f={k_f} k_s={k_s} k_cf={k_cf} k_v={k_v} k_va={k_va} {time.time() - t0:.0f}s", flush=True)
+    return "dense2048", "dense", out
+
+
 def job_c5_forward(_):
     t0 = time.time()
     z = np.load(os.path.join(OUT, "causal_128.npz"))
@@ -105,8 +129,10 @@ def job_c5_forward(_):
 
 
 def main():
-    which = sys.argv[1:] or ["c3", "c4", "c5"]
+    which = sys.argv[1:] or ["c3", "c4", "c5", "dense"]
     jobs = []
+    if "dense" in which:
+        jobs.append((job_dense, None))
     if "c3" in which:
         jobs += [(job_irl, ("c3", 128, 64, b, 3, False)) for b in (0, 63)]
     if "c4" in which:
@@ -118,6 +144,11 @@ def main():
         res = [r.get() for r in res]
     files = {}
     for cfg, key, out in res:
+        if key == "dense":
+            path = os.path.join(OUT, f"{cfg}.npz")
+            np.savez_compressed(path, **out)
+            print("wrote", path, os.path.getsize(path), "bytes")
+            continue
         d = files.setdefault(cfg, {})
         for k, v in out.items():
             d[f"{key}__{k}" if key != "fwd" else f"fwd__{k}"] = v
