@@ -943,12 +943,21 @@ static DenseBufs dense_bufs(const Ws& ws) {
 }
 
 // Shared table, B instances: the collapsed backward sweep is the GEMM
-// M [S x S] . ZS [S x B].  From IRLMX_DENSE_GEMM_MIN instances on (default
-// kDenseGemmMin, measured: DESIGN.md) it runs as one library dgemm (fp64 MFMA)
-// plus an epilogue instead of streaming M once per instance on the VALU.
-constexpr int kDenseGemmMin = 4;
+// M [S x S] . ZS [S x B].  Measured on MI355X (tools/diag/dense_bench.py,
+// profiles/r02_dense_kernel_stats.csv): streaming M once per instance on the
+// VALU re-reads it from the 256 MB last-level cache, so it wins until M leaves
+// that cache and B is large -- S = 2048: 10.8 / 16.4 / 36.6 / 102 us per sweep
+// at B = 1 / 4 / 16 / 64 against 118 us for the library dgemm at every B;
+// S = 4096, B = 64: 1170 us streaming against 452 us dgemm.  So the dgemm
+// (fp64 MFMA) runs from kDenseGemmMinStates states and kDenseGemmMinBatch
+// instances on; IRLMX_DENSE_GEMM_MIN=<B> forces the batch threshold alone.
+constexpr int kDenseGemmMinStates = 4096;
+constexpr int kDenseGemmMinBatch = 32;
 static bool dense_gemm(const Model& m) {
-  return m.dense && m.shared && m.B >= getenv_int("IRLMX_DENSE_GEMM_MIN", kDenseGemmMin);
+  if (!m.dense || !m.shared) return false;
+  const int forced = getenv_int("IRLMX_DENSE_GEMM_MIN", 0);
+  if (forced > 0) return m.B >= forced;
+  return m.S >= kDenseGemmMinStates && m.B >= kDenseGemmMinBatch;
 }
 
 // one rocBLAS handle per host thread and device (handles are not thread safe)

@@ -117,8 +117,9 @@ def test_random_dense_2048_vs_dense_oracle(dev, dense2048):
 
 def test_shared_table_gemm_backward(dev, dense2048, monkeypatch):
     """One dense table, 16 reward vectors: the backward sweep as one dgemm over all
-    instances (plan "dense-gemm") equals the per-instance streaming kernel and the
-    oracle (instance 0 carries the fixture's reward)."""
+    instances (plan "dense-gemm", forced: at S = 2048 streaming is faster) equals the
+    per-instance streaming kernel and the oracle (instance 0 carries the
+    fixture's reward)."""
     from irlmx import DeviceMDP, ops
     P, r, term, p0, z = dense2048
     B = 16
@@ -126,6 +127,8 @@ def test_shared_table_gemm_backward(dev, dense2048, monkeypatch):
     rew = np.random.default_rng(16).uniform(0.0, 1.0, (B, P.shape[0]))
     rew[0] = r
     tm = ops.terminal_mask(term, P.shape[0], batch=B, device=dev)
+    assert ops.execution_plan(mdp, "backward")["shape"] == "dense"   # below the measured crossover
+    monkeypatch.setenv("IRLMX_DENSE_GEMM_MIN", "2")
     assert ops.execution_plan(mdp, "backward")["shape"] == "dense-gemm"
     pi_gemm = ops.backward_maxent(mdp, rew, tm).cpu().numpy()
     monkeypatch.setenv("IRLMX_DENSE_GEMM_MIN", "1000000")
