@@ -23,12 +23,12 @@ from collections import defaultdict
 KERNELS = {"backward": "cluster_kernel<1", "forward": "cluster_kernel<0"}
 
 
-def main(tag, src, dst="profiles"):
+def main(tag, src, dst="profiles", config="c3"):
     os.makedirs(dst, exist_ok=True)
     stats = os.path.join(src, "kt", "kt_kernel_stats.csv")
     shutil.copy(stats, os.path.join(dst, f"{tag}_kernel_stats.csv"))
     rows = list(csv.DictReader(open(stats)))
-    summary = {"tag": tag, "kernels": {}}
+    summary = {"tag": tag, "config": config, "kernels": {}}
     for r in rows:
         summary["kernels"][r["Name"]] = {"calls": int(r["Calls"]), "avg_ms": float(r["AverageNs"]) / 1e6,
                                          "min_ms": float(r["MinNs"]) / 1e6, "max_ms": float(r["MaxNs"]) / 1e6,
@@ -63,4 +63,4 @@ def main(tag, src, dst="profiles"):
 
 
 if __name__ == "__main__":
-    main(sys.argv[1], sys.argv[2], *(sys.argv[3:4]))
+    main(sys.argv[1], sys.argv[2], *(sys.argv[3:5]))

@@ -7,7 +7,7 @@
 set -e
 TAG=${1:-r01}
 shift || true
-ARGS=${@:-"--steps 2 --warmup 1 --no-cpu-baseline"}
+ARGS=${@:-"--steps 2 --warmup 1 --no-cpu-baseline --no-config1 --first-steps 0"}
 ROOT=$(pwd)
 OUT=$ROOT/gpurun_out/prof_$TAG
 mkdir -p $OUT
@@ -16,4 +16,6 @@ cd /tmp
 timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/kt -o kt -- python3 $ROOT/bench.py $ARGS > $OUT/bench_kt.json 2> $OUT/kt.err
 timeout -k 10 400 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $OUT/fetch -o fetch -- python3 $ROOT/bench.py $ARGS > $OUT/bench_fetch.json 2> $OUT/fetch.err
 timeout -k 10 400 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $OUT/write -o write -- python3 $ROOT/bench.py $ARGS > $OUT/bench_write.json 2> $OUT/write.err
-find $OUT -name "*.csv" | head -20
+# keep the merged-back tree small: the per-dispatch traces are not needed
+rm -f $OUT/kt/*kernel_trace* $OUT/kt/*memory_copy* 2>/dev/null || true
+find $OUT -name "*.csv"
