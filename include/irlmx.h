@@ -164,6 +164,8 @@ int irlmx_value_iteration(const irlmx_mdp* mdp, const double* reward, double dis
 #define IRLMX_SHAPE_SWEEP 2   /* one launch per sweep */
 #define IRLMX_SHAPE_DENSE 3   /* DENSE layout: one launch per sweep, matrix rows streamed per instance */
 #define IRLMX_SHAPE_DENSE_GEMM 4 /* DENSE, shared table: the backward sweep as one dgemm over all instances */
+#define IRLMX_SHAPE_GRID 5    /* soft VI / VI on large grids: one persistent launch, values exchanged per sweep
+                                 ([3] = workgroups per instance) */
 int irlmx_execution_plan(const irlmx_mdp* mdp, int32_t op, int64_t* plan);
 
 /*

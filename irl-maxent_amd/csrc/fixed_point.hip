@@ -27,6 +27,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <atomic>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -135,6 +136,13 @@ static size_t align256(size_t x) { return (x + 255) & ~size_t(255); }
 
 static bool use_fused(const Model& m, int op);
 
+// Persistent grid shape (soft VI / VI on stencil grids too large for one CU):
+// states per thread and workgroups per instance; false when it does not apply.
+struct GridPlan {
+  int spt, bpi, xcd;
+};
+static bool grid_plan(const Model& m, int op, GridPlan* out);
+
 static Ws carve(const Model& m, int op, void* base) {
   Ws w;
   size_t off = 0;
@@ -158,11 +166,14 @@ static Ws carve(const Model& m, int op, void* base) {
   w.iters = (int64_t*)take(B * sizeof(int64_t));
   w.ndone = (int32_t*)take(sizeof(int32_t) * 4);
   const bool cl = sweep && m.stencil && (op == IRLMX_OP_FORWARD || op == IRLMX_OP_BACKWARD);
-  // cluster halo exchange: [B][2][S] and [B][3][H] 16-byte granule pairs
-  w.gran = (unsigned long long*)take(cl ? 2 * B * S * 16 : 0);
-  w.sgran = (unsigned long long*)take(cl ? 3 * B * (size_t)m.H * 16 : 0);
+  GridPlan gp{0, 0, 0};
+  const bool gr = sweep && (op == IRLMX_OP_SOFT_BACKWARD || op == IRLMX_OP_VALUE_ITERATION) && grid_plan(m, op, &gp);
+  // cluster halo exchange: [B][2][S] and [B][3][H] 16-byte granule pairs;
+  // grid shape: [B][3][S] value and [B][3][bpi] block-delta granules
+  w.gran = (unsigned long long*)take(cl ? 2 * B * S * 16 : (gr ? 3 * B * S * 16 : 0));
+  w.sgran = (unsigned long long*)take(cl ? 3 * B * (size_t)m.H * 16 : (gr ? 4 * B * (size_t)gp.bpi * 16 : 0));
   w.growth = (unsigned long long*)take(cl ? B * sizeof(unsigned long long) : 0);
-  w.err = (int*)take(cl ? 4 * sizeof(int) : 0);
+  w.err = (int*)take(cl || gr ? 4 * sizeof(int) : 0);
   w.total = off;
   return w;
 }
@@ -773,6 +784,253 @@ __global__ void bellman_finish_kernel(SoftArgs a, Ws ws) {
   if (s == 0 && a.iters) a.iters[b] = it;
 }
 
+// ---------------------------------------------------------------------------
+// persistent grid shape: soft VI / VI on stencil grids with S > 4096
+// ---------------------------------------------------------------------------
+//
+// One launch runs the whole loop.  Every workgroup owns SPT * kGridThreads
+// states of one instance, keeps their weights, reward and terminal reward in
+// registers, and exchanges values with the rest of the instance every sweep
+// through tagged granules in HBM (cluster.h: one 16-byte write-through store
+// {lo, tag, hi, tag} per value, tag = call salt | sweep; readers poll their
+// five stencil neighbours with sc1 loads until the tags match -- the data is
+// the flag, one fabric round trip per sweep and no global barrier).  The
+// convergence word travels the same way: each workgroup publishes the max
+// |v_new - v_old| of its states as one granule, and with sweep k's neighbour
+// values every workgroup also gathers all of sweep k's block maxima, so all of
+// them take the reference's decision (`while delta > eps`, NaN included: the
+// maxima are ordered bits, fixed_point.hip header) at the same sweep.  Values
+// and maxima live in rings of three sweeps: a workgroup can only write sweep
+// k + 3 after every workgroup of the instance has published sweep k + 2, i.e.
+// finished reading sweep k.  Per-state arithmetic is bellman_update's, in the
+// same order: results bit-identical to the fused and per-sweep shapes.
+constexpr int kGridThreads = 256;
+constexpr int kGridMaxActions = 5;
+
+struct GridArgs {
+  unsigned long long* gran;   // [B][3][S] x 16 B
+  unsigned long long* dgran;  // [B][4][bpi] x 16 B: three sweeps of block maxima + the XCC ids
+  int* err;
+  int bpi;
+  int nb;                     // instances
+  int xcd_group;              // workgroups dealt to XCD groups (see the kernel)
+  unsigned salt;
+};
+
+template <bool SOFT, int SPT>
+__global__ void __launch_bounds__(kGridThreads) bellman_grid_kernel(SoftArgs a, GridArgs g) {
+  const Model& m = a.m;
+  const int S = m.S, A = m.A;
+  // XCD grouping (as cluster.hip): workgroups are dealt round-robin over the 8
+  // XCDs, so the workgroups of instance g + 8 j are all taken from XCD group g
+  // and its hand-offs can stay in one L2 (checked below; speed only).  The grid
+  // is padded to 8 equal groups; padding workgroups leave at once.
+  int lin = blockIdx.x;
+  if (g.xcd_group) {
+    const int grp = blockIdx.x % 8, kk = blockIdx.x / 8;
+    const int il = grp + 8 * (kk / g.bpi);
+    if (il >= g.nb) return;
+    lin = il * g.bpi + kk % g.bpi;
+  }
+  const int b = lin / g.bpi, blk = lin % g.bpi, tid = threadIdx.x;
+  constexpr int K = kStencilK;
+  __shared__ unsigned long long red_in[kGridThreads / kWave], red_out[kGridThreads / kWave];
+  __shared__ int lflag;
+  int sidx[SPT];
+  bool ok[SPT];
+  int nb[SPT][K];
+  double w[SPT][kGridMaxActions][K];
+  double r[SPT], phi[SPT], cur[SPT], q[SPT][kGridMaxActions];
+  const double v0 = SOFT ? -1e200 : 0.0;  // maxent.py:323 / solver.py:32
+#pragma unroll
+  for (int j = 0; j < SPT; ++j) {
+    const int s = (blk * SPT + j) * kGridThreads + tid;
+    sidx[j] = s;
+    ok[j] = s < S;
+    const int ss = ok[j] ? s : 0;
+    r[j] = a.reward[(size_t)b * S + ss];
+    phi[j] = SOFT ? a.phi[(size_t)b * S + ss] : 0.0;
+    cur[j] = v0;
+#pragma unroll
+    for (int k = 0; k < K; ++k) nb[j][k] = stencil_nbr(ss, k, m.W, m.H);
+#pragma unroll
+    for (int act = 0; act < kGridMaxActions; ++act) {
+      q[j][act] = 0.0;
+#pragma unroll
+      for (int k = 0; k < K; ++k) w[j][act][k] = act < A ? row_val(m, b, act, k, ss) : 0.0;
+    }
+  }
+  if (tid == 0) lflag = 0;
+  const __amdgpu_buffer_rsrc_t rg = gran_rsrc(g.gran + (size_t)b * 6 * S, 48u * (unsigned)S);
+  const __amdgpu_buffer_rsrc_t rd = gran_rsrc(g.dgran + (size_t)b * 8 * g.bpi, 64u * (unsigned)g.bpi);
+  const unsigned salt = (g.salt & 0xFFFu) << 20;
+  // hand-off store form: write-through (sc1) in general; plain stores (kept in the
+  // XCD's L2, where the readers' sc1 loads are served) when every workgroup of
+  // the instance runs on the same XCD -- found by exchanging XCC ids once
+  bool plain = false;
+  {
+    unsigned xcc;
+    asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
+    xcc &= 0xFu;
+    const unsigned htag = salt | 0xFFFFFu;
+    if (tid == 0) gran_store(rd, (3u * (unsigned)g.bpi + (unsigned)blk) * 16u, xcc, htag, false);
+    unsigned off[1] = {(3u * (unsigned)g.bpi + (unsigned)tid) * 16u};
+    unsigned long long v[1] = {xcc};
+    if (!gran_gather<1>(rd, rd, off, tid < g.bpi ? 1u : 0u, htag, v)) lflag = 1;
+    const unsigned long long diff = wave_or_u64(tid < g.bpi ? (v[0] ^ xcc) : 0ull);
+    if ((tid & (kWave - 1)) == 0) red_in[tid / kWave] = diff;
+    __syncthreads();
+    if (lflag) {
+      if (tid == 0) atomicOr(g.err, 1);
+      return;
+    }
+    unsigned long long any = 0ull;
+#pragma unroll
+    for (int i = 0; i < kGridThreads / kWave; ++i) any |= red_in[i];
+    plain = g.xcd_group && any == 0ull;
+    __syncthreads();
+  }
+  double delta = 0.0;
+  long long k = 0;  // sweeps done: cur = v_k
+  for (;;) {
+    double nv[SPT][K];
+    if (k == 0) {
+#pragma unroll
+      for (int j = 0; j < SPT; ++j)
+#pragma unroll
+        for (int kk = 0; kk < K; ++kk) nv[j][kk] = v0;
+    } else {
+      // sweep k's neighbour values and (threads < bpi) all block maxima, one round trip
+      const unsigned tag = salt | ((unsigned)k & 0xFFFFFu);
+      const unsigned slot = (unsigned)(k % 3);
+      unsigned off[SPT * K + 1];
+      unsigned want = 0;
+#pragma unroll
+      for (int j = 0; j < SPT; ++j)
+#pragma unroll
+        for (int kk = 0; kk < K; ++kk) {
+          off[j * K + kk] = (slot * (unsigned)S + (unsigned)nb[j][kk]) * 16u;
+          want |= (ok[j] ? 1u : 0u) << (j * K + kk);
+        }
+      off[SPT * K] = (slot * (unsigned)g.bpi + (unsigned)tid) * 16u;
+      want |= (tid < g.bpi ? 1u : 0u) << (SPT * K);
+      unsigned long long v[SPT * K + 1];
+      if (!gran_gather<SPT * K + 1>(rg, rd, off, want, tag, v)) lflag = 1;
+#pragma unroll
+      for (int j = 0; j < SPT; ++j)
+#pragma unroll
+        for (int kk = 0; kk < K; ++kk) nv[j][kk] = ok[j] ? bits_double(v[j * K + kk]) : 0.0;
+      unsigned long long d = tid < g.bpi ? v[SPT * K] : 0ull;
+      d = wave_max_u64(d);
+      if ((tid & (kWave - 1)) == 0) red_in[tid / kWave] = d;
+      __syncthreads();
+      if (lflag) {
+        if (tid == 0) atomicOr(g.err, 1);
+        return;
+      }
+      unsigned long long mx = 0ull;
+#pragma unroll
+      for (int i = 0; i < kGridThreads / kWave; ++i) mx = red_in[i] > mx ? red_in[i] : mx;
+      delta = bits_double(mx);
+      if (!(delta > a.eps) || (a.max_iter > 0 && k >= a.max_iter)) break;  // maxent.py:326 / solver.py:40
+    }
+    // sweep k + 1 (bellman_update's arithmetic and order)
+    unsigned long long dmax = 0ull;
+    const unsigned tag1 = salt | ((unsigned)(k + 1) & 0xFFFFFu);
+    const unsigned slot1 = (unsigned)((k + 1) % 3);
+#pragma unroll
+    for (int j = 0; j < SPT; ++j) {
+      double v = SOFT ? phi[j] : 0.0;
+#pragma unroll
+      for (int act = 0; act < kGridMaxActions; ++act) {
+        if (act >= A) break;
+        double dot = 0.0;
+#pragma unroll
+        for (int kk = 0; kk < K; ++kk) dot = fma(w[j][act][kk], nv[j][kk], dot);
+        if (SOFT) {
+          q[j][act] = __dadd_rn(r[j], __dmul_rn(a.discount, dot));
+          v = softmax2(v, q[j][act]);  // maxent.py:329-333
+        } else {
+          const double qq = __dmul_rn(a.discount, dot);  // solver.py:44
+          if (a.average) v = act == 0 ? qq : __dadd_rn(v, qq);
+          else v = act == 0 ? qq : ((v != v || qq <= v) ? v : qq);
+        }
+      }
+      if (!SOFT) v = __dadd_rn(r[j], a.average ? v / (double)A : v);  // solver.py:47 / :99
+      if (ok[j]) {
+        const unsigned long long d = abs_bits(v - cur[j]);
+        dmax = d > dmax ? d : dmax;
+        gran_store(rg, (slot1 * (unsigned)S + (unsigned)sidx[j]) * 16u, dbits(v), tag1, plain);
+      }
+      cur[j] = v;
+    }
+    dmax = wave_max_u64(dmax);
+    if ((tid & (kWave - 1)) == 0) red_out[tid / kWave] = dmax;
+    __syncthreads();
+    if (tid == 0) {
+      unsigned long long mx = 0ull;
+      for (int i = 0; i < kGridThreads / kWave; ++i) mx = red_out[i] > mx ? red_out[i] : mx;
+      gran_store(rd, (slot1 * (unsigned)g.bpi + (unsigned)blk) * 16u, mx, tag1, plain);
+    }
+    ++k;
+  }
+#pragma unroll
+  for (int j = 0; j < SPT; ++j) {
+    if (!ok[j]) continue;
+    const size_t o = (size_t)b * S + sidx[j];
+    if (a.value) a.value[o] = cur[j];
+    if (SOFT)
+      for (int act = 0; act < A; ++act) a.pi[o * A + act] = exp(q[j][act] - cur[j]);  // maxent.py:341
+  }
+  if (blk == 0 && tid == 0) {
+    if (a.iters) a.iters[b] = k;
+    a.status[b] = finish_status(delta, a.eps);
+  }
+}
+
+template <bool SOFT>
+static void* bellman_grid_fn(int spt) {
+  switch (spt) {
+    case 1: return (void*)&bellman_grid_kernel<SOFT, 1>;
+    case 2: return (void*)&bellman_grid_kernel<SOFT, 2>;
+    case 4: return (void*)&bellman_grid_kernel<SOFT, 4>;
+  }
+  return nullptr;
+}
+
+static int grid_capacity(void* fn) {
+  int dev = 0, cus = 0, per_cu = 0;
+  if (hipGetDevice(&dev) != hipSuccess) return 0;
+  if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess) return 0;
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, (const void*)fn, kGridThreads, 0) != hipSuccess) return 0;
+  return cus * per_cu;
+}
+
+// the smallest states-per-thread whose grid is co-resident (all workgroups must
+// run at once: they wait on each other's granules); IRLMX_GRID=0 disables
+static bool grid_plan(const Model& m, int op, GridPlan* out) {
+  if (op != IRLMX_OP_SOFT_BACKWARD && op != IRLMX_OP_VALUE_ITERATION) return false;
+  if (!m.stencil || m.A > kGridMaxActions || getenv_int("IRLMX_GRID", 1) == 0) return false;
+  const bool soft = op == IRLMX_OP_SOFT_BACKWARD;
+  for (int spt = 1; spt <= 4; spt *= 2) {
+    const int bpi = (m.S + spt * kGridThreads - 1) / (spt * kGridThreads);
+    if (bpi > kGridThreads) continue;  // the block maxima are gathered one per thread
+    const int cap = grid_capacity(soft ? bellman_grid_fn<true>(spt) : bellman_grid_fn<false>(spt));
+    // XCD groups: ceil(B / 8) instances per group, each group within one XCD's
+    // share -- only from 8 instances on: fewer would leave XCDs idle (one 128x128
+    // instance: soft VI 3.5 ms grouped on one XCD vs 3.1 ms spread, 812 sweeps)
+    const bool xcd = getenv_int("IRLMX_XCD_GROUP", 1) != 0 && cap >= 8 && m.B >= 8 &&
+                     (long long)((m.B + 7) / 8) * bpi <= cap / 8;
+    if (xcd || (long long)bpi * m.B <= cap) {
+      *out = GridPlan{spt, bpi, xcd ? 1 : 0};
+      return true;
+    }
+  }
+  return false;
+}
+
+static std::atomic<unsigned> g_grid_salt{1};
+
 __global__ void fill_kernel(double* p, size_t n, double v) {
   const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i < n) p[i] = v;
@@ -1057,6 +1315,17 @@ extern "C" int irlmx_execution_plan(const irlmx_mdp* mdp, int32_t op, int64_t* p
     plan[9] = (int64_t)cp.lds;
     return 0;
   }
+  GridPlan gp;
+  if (grid_plan(m, op, &gp)) {
+    plan[0] = IRLMX_SHAPE_GRID;
+    plan[2] = gp.xcd;   // (the G column: 1 = workgroups grouped by XCD)
+    plan[3] = gp.bpi;
+    plan[4] = m.B;
+    plan[5] = gp.spt;
+    plan[7] = kGridThreads;
+    plan[8] = 1;
+    return 0;
+  }
   if (m.dense) {
     plan[0] = (op == IRLMX_OP_BACKWARD && dense_gemm(m)) ? IRLMX_SHAPE_DENSE_GEMM : IRLMX_SHAPE_DENSE;
     plan[7] = kDenseThreads;
@@ -1197,6 +1466,10 @@ static int bellman_common(const irlmx_mdp* mdp, const double* reward, const doub
     return 0;
   }
   const dim3 g((m.S + kSweepThreads - 1) / kSweepThreads, m.B);
+  // the Bellman sweep is a latency chain per state (A dots, A softmax folds):
+  // smaller workgroups spread one instance over more CUs (IRLMX_BELLMAN_THREADS)
+  const int bt = std::max(64, std::min(kSweepThreads, getenv_int("IRLMX_BELLMAN_THREADS", kSweepThreads)));
+  const dim3 gb((m.S + bt - 1) / bt, m.B);
   const size_t n = (size_t)m.B * m.S;
   hipLaunchKernelGGL(fill_kernel, dim3((n + 255) / 256), dim3(256), 0, st, ws.buf0, n, soft ? -1e200 : 0.0);
   if (m.dense) {  // dense rows (dense.hip)
@@ -1210,9 +1483,24 @@ static int bellman_common(const irlmx_mdp* mdp, const double* reward, const doub
     e = hipGetLastError();
     return e == hipSuccess ? 0 : hip_fail(e, "dense bellman");
   }
+  GridPlan gp;
+  if (grid_plan(m, op, &gp)) {  // persistent grid shape: one launch for the whole loop
+    GridArgs ga{ws.gran, ws.sgran, ws.err, gp.bpi, m.B, gp.xcd, g_grid_salt.fetch_add(1, std::memory_order_relaxed)};
+    void* fn = soft ? bellman_grid_fn<true>(gp.spt) : bellman_grid_fn<false>(gp.spt);
+    void* args[] = {&a, &ga};
+    const int grid = gp.xcd ? 8 * ((m.B + 7) / 8) * gp.bpi : gp.bpi * m.B;
+    e = hipLaunchKernel(fn, dim3(grid), dim3(kGridThreads), args, 0, st);
+    if (e != hipSuccess) return hip_fail(e, "bellman grid launch");
+    int err = 0;
+    e = hipMemcpyAsync(&err, ws.err, sizeof(int), hipMemcpyDeviceToHost, st);
+    if (e == hipSuccess) e = hipStreamSynchronize(st);
+    if (e != hipSuccess) return hip_fail(e, "bellman grid sync");
+    if (err) { set_error("bellman grid: exchange timed out (workgroups not co-resident?)"); return IRLMX_EHIP; }
+    return 0;
+  }
   int rc = run_until_done(ws, m.B, st, [&](long long it, int r3) {
-    if (soft) hipLaunchKernelGGL(bellman_sweep_kernel<true>, g, dim3(kSweepThreads), 0, st, a, ws, it, r3);
-    else hipLaunchKernelGGL(bellman_sweep_kernel<false>, g, dim3(kSweepThreads), 0, st, a, ws, it, r3);
+    if (soft) hipLaunchKernelGGL(bellman_sweep_kernel<true>, gb, dim3(bt), 0, st, a, ws, it, r3);
+    else hipLaunchKernelGGL(bellman_sweep_kernel<false>, gb, dim3(bt), 0, st, a, ws, it, r3);
   });
   if (rc) return rc;
   if (soft) hipLaunchKernelGGL(bellman_finish_kernel<true>, g, dim3(kSweepThreads), 0, st, a, ws);

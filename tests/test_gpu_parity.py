@@ -621,3 +621,31 @@ def test_dense_to_ell_device(dev):
             exp_c = np.concatenate([P[src, s, :].T, np.zeros((A, k_col - src.size))], axis=1)
             assert np.array_equal(cv[:, :, s], exp_c), (S, s)
         assert np.array_equal(mdp.to_dense(), P)
+
+
+@pytest.mark.parametrize("size,batch", [(128, 1), (128, 5), (256, 2)])
+def test_grid_shape_soft_vi_and_vi_bit_identical(dev, monkeypatch, size, batch):
+    """Soft VI (maxent.py:326-338) and VI (solver.py:40-50, 95-100) on the
+    persistent grid shape (one launch; values and block maxima exchanged every
+    sweep as tagged granules) against the per-sweep shape: identical sweep
+    counts and status, values and policies bit for bit."""
+    from irlmx import DeviceMDP, ops
+    from irlmx.batch import terminal_reward
+    n = size * size
+    mdp = DeviceMDP.icy_gridworld(size, list(np.linspace(0.1, 0.3, batch)), device=dev)
+    r = np.random.default_rng(size + batch).uniform(0.0, 1.5, (batch, n))
+    phi = terminal_reward([n - 1], n, batch, dev)
+    assert ops.execution_plan(mdp, "soft_backward")["shape"] == "grid"
+    assert ops.execution_plan(mdp, "value_iteration")["shape"] == "grid"
+    soft = ops.soft_backward(mdp, r, phi, 0.7)
+    vi = ops.value_iteration(mdp, r, 0.9)
+    via = ops.value_iteration(mdp, r, 0.9, average=True)
+    monkeypatch.setenv("IRLMX_GRID", "0")
+    assert ops.execution_plan(mdp, "soft_backward")["shape"] == "sweep"
+    soft0 = ops.soft_backward(mdp, r, phi, 0.7)
+    vi0 = ops.value_iteration(mdp, r, 0.9)
+    via0 = ops.value_iteration(mdp, r, 0.9, average=True)
+    for got, ref in ((soft, soft0), (vi, vi0), (via, via0)):
+        for x, y in zip(got, ref):
+            assert torch.equal(x.view(torch.int64) if x.dtype == torch.float64 else x,
+                               y.view(torch.int64) if y.dtype == torch.float64 else y)

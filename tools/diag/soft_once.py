@@ -16,3 +16,9 @@ for _ in range(2):
     pi, v, k, st = ops.soft_backward(mdp, r, phi, 0.7)
     torch.cuda.synchronize()
     print(f"soft VI {int(k[0])} sweeps {1e3 * (time.perf_counter() - t):.2f} ms", flush=True)
+
+v, kv, _ = ops.value_iteration(mdp, r, 0.9)
+torch.cuda.synchronize(); t = time.perf_counter()
+v, kv, _ = ops.value_iteration(mdp, r, 0.9)
+torch.cuda.synchronize()
+print(f"VI {int(kv[0])} sweeps {1e3 * (time.perf_counter() - t):.2f} ms", flush=True)
