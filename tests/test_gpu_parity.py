@@ -649,3 +649,32 @@ def test_grid_shape_soft_vi_and_vi_bit_identical(dev, monkeypatch, size, batch):
         for x, y in zip(got, ref):
             assert torch.equal(x.view(torch.int64) if x.dtype == torch.float64 else x,
                                y.view(torch.int64) if y.dtype == torch.float64 else y)
+
+
+def test_grid_shape_cap_and_nonfinite(dev, monkeypatch):
+    """Grid shape edge cases against the per-sweep shape: a sweep cap (status
+    MAXITER at the cap), a NaN reward in one instance (NaN delta stops its loop
+    at once, status NONFINITE, as `while NaN > eps` does) next to a finite one."""
+    from irlmx import DeviceMDP, ops
+    from irlmx.batch import terminal_reward
+    size, batch = 128, 2
+    n = size * size
+    mdp = DeviceMDP.icy_gridworld(size, [0.2, 0.2], device=dev)
+    r = np.random.default_rng(3).uniform(0.0, 1.5, (batch, n))
+    r[1, 777] = np.nan
+    phi = terminal_reward([n - 1], n, batch, dev)
+
+    def run():
+        return (ops.soft_backward(mdp, r, phi, 0.7, max_iter=50), ops.soft_backward(mdp, r, phi, 0.7),
+                ops.value_iteration(mdp, r, 0.9, max_iter=7))
+
+    assert ops.execution_plan(mdp, "soft_backward")["shape"] == "grid"
+    got = run()
+    assert int(got[0][2][0]) == 50 and int(got[0][3][0]) == 2            # capped: IRLMX_MAXITER
+    assert int(got[1][3][1]) == 1 and int(got[1][3][0]) == 0              # NaN instance: NONFINITE
+    monkeypatch.setenv("IRLMX_GRID", "0")
+    ref = run()
+    for g_, r_ in zip(got, ref):
+        for x, y in zip(g_, r_):
+            assert torch.equal(x.view(torch.int64) if x.dtype == torch.float64 else x,
+                               y.view(torch.int64) if y.dtype == torch.float64 else y)
