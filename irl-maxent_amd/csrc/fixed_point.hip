@@ -817,10 +817,10 @@ struct GridArgs {
   unsigned salt;
 };
 
-template <bool SOFT, int SPT>
+template <bool SOFT, int SPT, int KMAX>
 __global__ void __launch_bounds__(kGridThreads) bellman_grid_kernel(SoftArgs a, GridArgs g) {
   const Model& m = a.m;
-  const int S = m.S, A = m.A;
+  const int S = m.S, A = m.A, Kr = m.K;  // Kr <= KMAX slots: the stencil's five or the ELL row form's
   // XCD grouping (as cluster.hip): workgroups are dealt round-robin over the 8
   // XCDs, so the workgroups of instance g + 8 j are all taken from XCD group g
   // and its hand-offs can stay in one L2 (checked below; speed only).  The grid
@@ -833,7 +833,7 @@ __global__ void __launch_bounds__(kGridThreads) bellman_grid_kernel(SoftArgs a, 
     lin = il * g.bpi + kk % g.bpi;
   }
   const int b = lin / g.bpi, blk = lin % g.bpi, tid = threadIdx.x;
-  constexpr int K = kStencilK;
+  constexpr int K = KMAX;
   __shared__ unsigned long long red_in[kGridThreads / kWave], red_out[kGridThreads / kWave];
   __shared__ int lflag;
   int sidx[SPT];
@@ -852,12 +852,12 @@ __global__ void __launch_bounds__(kGridThreads) bellman_grid_kernel(SoftArgs a, 
     phi[j] = SOFT ? a.phi[(size_t)b * S + ss] : 0.0;
     cur[j] = v0;
 #pragma unroll
-    for (int k = 0; k < K; ++k) nb[j][k] = stencil_nbr(ss, k, m.W, m.H);
+    for (int k = 0; k < K; ++k) nb[j][k] = k < Kr ? row_nbr(m, b, ss, k) : ss;
 #pragma unroll
     for (int act = 0; act < kGridMaxActions; ++act) {
       q[j][act] = 0.0;
 #pragma unroll
-      for (int k = 0; k < K; ++k) w[j][act][k] = act < A ? row_val(m, b, act, k, ss) : 0.0;
+      for (int k = 0; k < K; ++k) w[j][act][k] = (act < A && k < Kr) ? row_val(m, b, act, k, ss) : 0.0;
     }
   }
   if (tid == 0) lflag = 0;
@@ -910,7 +910,7 @@ __global__ void __launch_bounds__(kGridThreads) bellman_grid_kernel(SoftArgs a, 
 #pragma unroll
         for (int kk = 0; kk < K; ++kk) {
           off[j * K + kk] = (slot * (unsigned)S + (unsigned)nb[j][kk]) * 16u;
-          want |= (ok[j] ? 1u : 0u) << (j * K + kk);
+          want |= (ok[j] && kk < Kr ? 1u : 0u) << (j * K + kk);
         }
       off[SPT * K] = (slot * (unsigned)g.bpi + (unsigned)tid) * 16u;
       want |= (tid < g.bpi ? 1u : 0u) << (SPT * K);
@@ -919,7 +919,7 @@ __global__ void __launch_bounds__(kGridThreads) bellman_grid_kernel(SoftArgs a, 
 #pragma unroll
       for (int j = 0; j < SPT; ++j)
 #pragma unroll
-        for (int kk = 0; kk < K; ++kk) nv[j][kk] = ok[j] ? bits_double(v[j * K + kk]) : 0.0;
+        for (int kk = 0; kk < K; ++kk) nv[j][kk] = (ok[j] && kk < Kr) ? bits_double(v[j * K + kk]) : 0.0;
       unsigned long long d = tid < g.bpi ? v[SPT * K] : 0ull;
       d = wave_max_u64(d);
       if ((tid & (kWave - 1)) == 0) red_in[tid / kWave] = d;
@@ -946,7 +946,8 @@ __global__ void __launch_bounds__(kGridThreads) bellman_grid_kernel(SoftArgs a, 
         if (act >= A) break;
         double dot = 0.0;
 #pragma unroll
-        for (int kk = 0; kk < K; ++kk) dot = fma(w[j][act][kk], nv[j][kk], dot);
+        for (int kk = 0; kk < K; ++kk)
+          if (kk < Kr) dot = fma(w[j][act][kk], nv[j][kk], dot);
         if (SOFT) {
           q[j][act] = __dadd_rn(r[j], __dmul_rn(a.discount, dot));
           v = softmax2(v, q[j][act]);  // maxent.py:329-333
@@ -989,14 +990,22 @@ __global__ void __launch_bounds__(kGridThreads) bellman_grid_kernel(SoftArgs a, 
 }
 
 template <bool SOFT>
-static void* bellman_grid_fn(int spt) {
-  switch (spt) {
-    case 1: return (void*)&bellman_grid_kernel<SOFT, 1>;
-    case 2: return (void*)&bellman_grid_kernel<SOFT, 2>;
-    case 4: return (void*)&bellman_grid_kernel<SOFT, 4>;
+static void* bellman_grid_fn(int spt, int kmax) {
+  if (kmax == 5) {
+    switch (spt) {
+      case 1: return (void*)&bellman_grid_kernel<SOFT, 1, 5>;
+      case 2: return (void*)&bellman_grid_kernel<SOFT, 2, 5>;
+      case 4: return (void*)&bellman_grid_kernel<SOFT, 4, 5>;
+    }
+  } else if (kmax == 8) {
+    switch (spt) {
+      case 1: return (void*)&bellman_grid_kernel<SOFT, 1, 8>;
+      case 2: return (void*)&bellman_grid_kernel<SOFT, 2, 8>;
+    }
   }
   return nullptr;
 }
+static int grid_kmax(const Model& m) { return m.K <= 5 ? 5 : (m.K <= 8 ? 8 : 0); }
 
 static int grid_capacity(void* fn) {
   int dev = 0, cus = 0, per_cu = 0;
@@ -1010,12 +1019,15 @@ static int grid_capacity(void* fn) {
 // run at once: they wait on each other's granules); IRLMX_GRID=0 disables
 static bool grid_plan(const Model& m, int op, GridPlan* out) {
   if (op != IRLMX_OP_SOFT_BACKWARD && op != IRLMX_OP_VALUE_ITERATION) return false;
-  if (!m.stencil || m.A > kGridMaxActions || getenv_int("IRLMX_GRID", 1) == 0) return false;
+  if (m.dense || m.A > kGridMaxActions || !grid_kmax(m) || getenv_int("IRLMX_GRID", 1) == 0) return false;
+  if (m.S <= fused_max_states()) return false;  // one workgroup holds it: the fused shape
   const bool soft = op == IRLMX_OP_SOFT_BACKWARD;
   for (int spt = 1; spt <= 4; spt *= 2) {
+    void* fn = soft ? bellman_grid_fn<true>(spt, grid_kmax(m)) : bellman_grid_fn<false>(spt, grid_kmax(m));
+    if (!fn) continue;
     const int bpi = (m.S + spt * kGridThreads - 1) / (spt * kGridThreads);
     if (bpi > kGridThreads) continue;  // the block maxima are gathered one per thread
-    const int cap = grid_capacity(soft ? bellman_grid_fn<true>(spt) : bellman_grid_fn<false>(spt));
+    const int cap = grid_capacity(fn);
     // XCD groups: ceil(B / 8) instances per group, each group within one XCD's
     // share -- only from 8 instances on: fewer would leave XCDs idle (one 128x128
     // instance: soft VI 3.5 ms grouped on one XCD vs 3.1 ms spread, 812 sweeps)
@@ -1486,7 +1498,7 @@ static int bellman_common(const irlmx_mdp* mdp, const double* reward, const doub
   GridPlan gp;
   if (grid_plan(m, op, &gp)) {  // persistent grid shape: one launch for the whole loop
     GridArgs ga{ws.gran, ws.sgran, ws.err, gp.bpi, m.B, gp.xcd, g_grid_salt.fetch_add(1, std::memory_order_relaxed)};
-    void* fn = soft ? bellman_grid_fn<true>(gp.spt) : bellman_grid_fn<false>(gp.spt);
+    void* fn = soft ? bellman_grid_fn<true>(gp.spt, grid_kmax(m)) : bellman_grid_fn<false>(gp.spt, grid_kmax(m));
     void* args[] = {&a, &ga};
     const int grid = gp.xcd ? 8 * ((m.B + 7) / 8) * gp.bpi : gp.bpi * m.B;
     e = hipLaunchKernel(fn, dim3(grid), dim3(kGridThreads), args, 0, st);

@@ -49,7 +49,7 @@ def dev():
     return irlmx.require_device()
 
 
-@pytest.fixture(params=["fused", "sweep", "cluster"])
+@pytest.fixture(params=["fused", "sweep", "cluster", "grid"])
 def shape(request, monkeypatch):
     """Run each case through every execution shape of the kernels.
 
@@ -58,12 +58,16 @@ def shape(request, monkeypatch):
     cluster : persistent tiles of 3 rows with 2 ghost rows (forced small so the
               golden cases exercise the halo exchange, the in-block rollback of
               the forward pass and the block-boundary rescaling of the backward)
+    grid    : soft VI / VI as one persistent launch exchanging values every sweep
+              (forward / backward: the per-sweep shape)
     """
-    for k in ("IRLMX_FUSED_MAX_STATES", "IRLMX_CLUSTER", "IRLMX_CLUSTER_R", "IRLMX_CLUSTER_G"):
+    for k in ("IRLMX_FUSED_MAX_STATES", "IRLMX_CLUSTER", "IRLMX_CLUSTER_R", "IRLMX_CLUSTER_G", "IRLMX_GRID"):
         monkeypatch.delenv(k, raising=False)
-    if request.param == "sweep":
+    if request.param in ("sweep", "grid"):
         monkeypatch.setenv("IRLMX_FUSED_MAX_STATES", "0")
         monkeypatch.setenv("IRLMX_CLUSTER", "0")
+        if request.param == "sweep":
+            monkeypatch.setenv("IRLMX_GRID", "0")
     elif request.param == "cluster":
         monkeypatch.setenv("IRLMX_FUSED_MAX_STATES", "0")
         monkeypatch.setenv("IRLMX_CLUSTER_R", "3")
@@ -236,7 +240,7 @@ def test_maxent_small_cases(dev, shape):
         mdp = DeviceMDP.icy_gridworld(size, float(z[c + "__p_slip"]), device=dev)
         tm = ops.terminal_mask(term, n, device=dev)
         ref_pi = z[c + "__pi"]
-        if shape == "sweep" and int(z[c + "__k_f"]) > 100_000:
+        if shape in ("sweep", "grid") and int(z[c + "__k_f"]) > 100_000:
             continue  # millions of one-sweep launches; the fused and cluster shapes cover it
         if np.isfinite(ref_pi).all():
             pi = ops.backward_maxent(mdp, z[c + "__reward"], tm)

@@ -204,3 +204,39 @@ def test_sparse_value_iteration_matches_dense():
             v, k = O.value_iteration(P, r, 0.9, average=avg)
             vs, ks = O.value_iteration_csr(mats, r, 0.9, average=avg)
             assert k == ks and np.max(np.abs(vs - v)) <= 1e-12 * np.max(np.abs(v))
+
+
+def test_full_size_fixtures_consistent():
+    """The converged full-size fixtures (tools/gen_full_fixtures.py) are what the
+    oracle's own loops produce: their inputs regenerate bit for bit (bench slips,
+    demonstrations from the oracle's STENCIL5 table, the seeded dense MDP), and a
+    short re-run of the CSR irl restatement on a 16x16 version of the bench
+    workload matches the dense oracle's loop."""
+    import numpy as np
+    from irlmx import demos
+    for cfg, size, total in (("c3", 128, 64), ("c4", 256, 32), ("c5", 128, 1)):
+        z = load_golden(f"full_{cfg}")
+        b = int(z["instances"][0])
+        slip = 0.1 + 0.2 * b / total
+        assert float(z[f"{b}__slip"]) == slip
+        n = size * size
+        e_f, p0, _ = demos.sample(O.stencil_row_val(O.icy_gridworld_csr(size, slip), size), size, [n - 1], 0,
+                                  n=200, seed=1234 + b)
+        assert np.array_equal(e_f, z[f"{b}__e_f"]) and np.array_equal(p0, z[f"{b}__p0"])
+    z = load_golden("dense2048")
+    P, r, term, p0 = O.random_dense_mdp()
+    assert np.array_equal(np.array([P.sum(), P[::7, ::5, :].sum(), P[-1, -1, -1]]), z["P_check"])
+    assert np.array_equal(r, z["reward"])
+    # the CSR irl steps restate the dense loop (maxent.py:240-252) on a small grid
+    size, n = 16, 256
+    mats = O.icy_gridworld_csr(size, 0.15)
+    e_f, p0, _ = demos.sample(O.stencil_row_val(mats, size), size, [n - 1], 0, n=50, seed=7)
+    res = O.irl_steps_csr(mats, e_f, p0, [n - 1], 3)
+    Pd = O.icy_gridworld_table(size, 0.15)
+    theta = np.ones(n)
+    for k in range(3):
+        pi = O.backward_maxent(Pd, [n - 1], theta, rescale=True)
+        svf, kf = O.forward_svf(Pd, p0, [n - 1], pi)
+        theta = theta * np.exp(0.2 / (1 + k) * (e_f - svf))
+        assert kf == res["k_f"][k]
+        assert np.max(np.abs(theta - res["theta"][k])) <= 1e-12 * np.max(np.abs(theta))
