@@ -385,6 +385,114 @@ dense_bellman_finish_kernel(DenseView d, DenseBellman a, DenseBufs w) {
 }
 
 // ---------------------------------------------------------------------------
+// batched GEMM on the fp64 matrix cores: C[b][s] = sum_t M[s][t] * Z[b][t]
+// ---------------------------------------------------------------------------
+//
+// One table shared by B instances (the backward sweep M . [zs_1 .. zs_B]).
+// v_mfma_f64_16x16x4_f64: lane l supplies A[l & 15][k = l >> 4] and
+// B[k = l >> 4][l & 15]; D[row (l >> 4) + 4 r][col l & 15] in register r
+// (cdna_hip_programming.md, f64 MFMA maps).  A workgroup owns 32 rows of M x 64
+// instances; its four waves split the sum over t (K) into quarters and meet in
+// LDS, summed in wave order (deterministic).  Per 16-wide K chunk a lane loads
+// 32 contiguous bytes of each of its rows of M and Z (128 B per row across the
+// four lanes of a column), and MFMA x (x = 0..3) uses element x of them: the
+// k index of both operands maps to the same t = 16 c + 4 (l >> 4) + x.  M is
+// read from HBM once per sweep; Z (B x S) is re-read per 32 rows of M (L2).
+constexpr int kGemmWaves = 4;
+
+typedef double f64x4 __attribute__((ext_vector_type(4)));
+
+// ST 16-row tiles of M and NBT 16-instance column tiles per workgroup (sized to
+// S and B so that the grid fills the chip)
+template <int ST, int NBT>
+__global__ void __launch_bounds__(kGemmWaves * kWave)
+dense_gemm_kernel(const double* __restrict__ M, const double* __restrict__ Z, double* __restrict__ C, int S, int B) {
+  extern __shared__ __attribute__((aligned(16))) double part[];  // [waves][ST][NBT][4][64]
+  const int wave = threadIdx.x / kWave, l = threadIdx.x & (kWave - 1);
+  const int s0 = blockIdx.x * 16 * ST, b0 = blockIdx.y * 16 * NBT;
+  const int i = l & 15, q = l >> 4;
+  const int nchunk = (S + 15) / 16;
+  const int c0 = wave * nchunk / kGemmWaves, c1 = (wave + 1) * nchunk / kGemmWaves;
+  f64x4 acc[ST][NBT];
+#pragma unroll
+  for (int st = 0; st < ST; ++st)
+#pragma unroll
+    for (int bt = 0; bt < NBT; ++bt) acc[st][bt] = f64x4{0.0, 0.0, 0.0, 0.0};
+  // rows of this lane (out of range: a valid row, zeroed on load)
+  const double* mrow[ST];
+  const double* zrow[NBT];
+  bool mok[ST], zok[NBT];
+#pragma unroll
+  for (int st = 0; st < ST; ++st) {
+    const int r = s0 + 16 * st + i;
+    mok[st] = r < S;
+    mrow[st] = M + (size_t)(mok[st] ? r : 0) * S;
+  }
+#pragma unroll
+  for (int bt = 0; bt < NBT; ++bt) {
+    const int r = b0 + 16 * bt + i;
+    zok[bt] = r < B;
+    zrow[bt] = Z + (size_t)(zok[bt] ? r : 0) * S;
+  }
+  // the 4 consecutive t of chunk c this lane supplies (S % 4 == 0: all in or all out)
+  double2 ma[ST][2], za[NBT][2];
+  auto load = [&](int c, double2 (&mo)[ST][2], double2 (&zo)[NBT][2]) {
+    const int t = 16 * c + 4 * q;
+    const bool tok = c < c1 && t < S;
+#pragma unroll
+    for (int st = 0; st < ST; ++st) {
+      mo[st][0] = mo[st][1] = make_double2(0.0, 0.0);
+      if (tok && mok[st]) {
+        mo[st][0] = *reinterpret_cast<const double2*>(mrow[st] + t);
+        mo[st][1] = *reinterpret_cast<const double2*>(mrow[st] + t + 2);
+      }
+    }
+#pragma unroll
+    for (int bt = 0; bt < NBT; ++bt) {
+      zo[bt][0] = zo[bt][1] = make_double2(0.0, 0.0);
+      if (tok && zok[bt]) {
+        zo[bt][0] = *reinterpret_cast<const double2*>(zrow[bt] + t);
+        zo[bt][1] = *reinterpret_cast<const double2*>(zrow[bt] + t + 2);
+      }
+    }
+  };
+  auto el = [](const double2 (&v)[2], int x) { return x == 0 ? v[0].x : x == 1 ? v[0].y : x == 2 ? v[1].x : v[1].y; };
+  load(c0, ma, za);
+  for (int c = c0; c < c1; ++c) {
+    double2 mn[ST][2], zn[NBT][2];
+    load(c + 1, mn, zn);  // next chunk in flight during this chunk's MFMAs
+#pragma unroll
+    for (int x = 0; x < 4; ++x)
+#pragma unroll
+      for (int st = 0; st < ST; ++st)
+#pragma unroll
+        for (int bt = 0; bt < NBT; ++bt)
+          acc[st][bt] = __builtin_amdgcn_mfma_f64_16x16x4f64(el(ma[st], x), el(za[bt], x), acc[st][bt], 0, 0, 0);
+#pragma unroll
+    for (int st = 0; st < ST; ++st) { ma[st][0] = mn[st][0]; ma[st][1] = mn[st][1]; }
+#pragma unroll
+    for (int bt = 0; bt < NBT; ++bt) { za[bt][0] = zn[bt][0]; za[bt][1] = zn[bt][1]; }
+  }
+  // split-K partials -> LDS, summed in wave order
+#pragma unroll
+  for (int st = 0; st < ST; ++st)
+#pragma unroll
+    for (int bt = 0; bt < NBT; ++bt)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) part[((((size_t)wave * ST + st) * NBT + bt) * 4 + r) * kWave + l] = acc[st][bt][r];
+  __syncthreads();
+  constexpr int kOut = ST * NBT * 4 * kWave;  // outputs per workgroup
+  for (int e = threadIdx.x; e < kOut; e += kGemmWaves * kWave) {
+    double v = part[e];
+#pragma unroll
+    for (int w = 1; w < kGemmWaves; ++w) v += part[(size_t)w * kOut + e];
+    const int ll = e % kWave, r = (e / kWave) % 4, bt = (e / (kWave * 4)) % NBT, st = e / (kWave * 4 * NBT);
+    const int row = s0 + 16 * st + (ll >> 4) + 4 * r, col = b0 + 16 * bt + (ll & 15);
+    if (row < S && col < B) C[(size_t)col * S + row] = v;
+  }
+}
+
+// ---------------------------------------------------------------------------
 // launchers
 // ---------------------------------------------------------------------------
 
@@ -463,6 +571,37 @@ void dense_bellman_finish_launch(const DenseView& d, const DenseBellman& a, Dens
                        w);
   else
     hipLaunchKernelGGL(dense_bellman_finish_kernel<false>, row_grid(d), dim3(kDenseThreads), 0, st, d, a, w);
+}
+
+}  // namespace irlmx
+
+namespace irlmx {
+
+bool dense_gemm_mfma_ok(int S) { return S % 4 == 0; }
+
+template <int ST, int NBT>
+static void gemm_go(const double* M, const double* Z, double* C, int S, int B, hipStream_t st) {
+  const size_t lds = (size_t)kGemmWaves * ST * NBT * 4 * kWave * sizeof(double);
+  (void)hipFuncSetAttribute((const void*)&dense_gemm_kernel<ST, NBT>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                            (int)lds);
+  const dim3 grid((S + 16 * ST - 1) / (16 * ST), (B + 16 * NBT - 1) / (16 * NBT));
+  hipLaunchKernelGGL((dense_gemm_kernel<ST, NBT>), grid, dim3(kGemmWaves * kWave), lds, st, M, Z, C, S, B);
+}
+
+void dense_gemm_launch(const double* M, const double* Z, double* C, int S, int B, hipStream_t st) {
+  const int nbt = B <= 16 ? 1 : (B <= 32 ? 2 : 4);
+  const int ny = (B + 16 * nbt - 1) / (16 * nbt);
+  // two row tiles per wave (half the Z re-reads) while that still gives >= 256 workgroups
+  const bool st2 = (long long)((S + 31) / 32) * ny >= 256;
+  if (st2) {
+    if (nbt == 1) gemm_go<2, 1>(M, Z, C, S, B, st);
+    else if (nbt == 2) gemm_go<2, 2>(M, Z, C, S, B, st);
+    else gemm_go<2, 4>(M, Z, C, S, B, st);
+  } else {
+    if (nbt == 1) gemm_go<1, 1>(M, Z, C, S, B, st);
+    else if (nbt == 2) gemm_go<1, 2>(M, Z, C, S, B, st);
+    else gemm_go<1, 4>(M, Z, C, S, B, st);
+  }
 }
 
 }  // namespace irlmx

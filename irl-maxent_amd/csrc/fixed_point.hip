@@ -1214,20 +1214,24 @@ static DenseBufs dense_bufs(const Ws& ws) {
 
 // Shared table, B instances: the collapsed backward sweep is the GEMM
 // M [S x S] . ZS [S x B].  Measured on MI355X (tools/diag/dense_bench.py,
-// profiles/r02_dense_kernel_stats.csv): streaming M once per instance on the
-// VALU re-reads it from the 256 MB last-level cache, so it wins until M leaves
-// that cache and B is large -- S = 2048: 10.8 / 16.4 / 36.6 / 102 us per sweep
-// at B = 1 / 4 / 16 / 64 against 118 us for the library dgemm at every B;
-// S = 4096, B = 64: 1170 us streaming against 452 us dgemm.  So the dgemm
-// (fp64 MFMA) runs from kDenseGemmMinStates states and kDenseGemmMinBatch
-// instances on; IRLMX_DENSE_GEMM_MIN=<B> forces the batch threshold alone.
-constexpr int kDenseGemmMinStates = 4096;
-constexpr int kDenseGemmMinBatch = 32;
+// profiles/r02_dense_gemm_bench.txt, microseconds per sweep):
+//
+//            streaming (VALU)      hand-written fp64 MFMA     rocBLAS dgemm
+//   S=2048   B=4 16  B=16 36  B=64 102   25 / 25 / 45           116 / 117 / 117
+//   S=4096   B=4 63  B=16 277 B=64 1173  48 / 47 / 85           448 / 447 / 451
+//
+// Streaming re-reads M from the 256 MB last-level cache, so it wins for few
+// instances while M is small; the MFMA kernel (dense.hip dense_gemm_kernel) wins
+// from 16 instances on, and from 4 on once M leaves that cache (S >= 4096).  The
+// library dgemm (fp64 MFMA kernels too, rocprof: Cijk_..._MI16x16x4x1) is the
+// fallback for S % 4 != 0 and is used only where it beats streaming.
+// IRLMX_DENSE_GEMM_MIN=<B> forces the batch threshold alone.
 static bool dense_gemm(const Model& m) {
   if (!m.dense || !m.shared) return false;
   const int forced = getenv_int("IRLMX_DENSE_GEMM_MIN", 0);
   if (forced > 0) return m.B >= forced;
-  return m.S >= kDenseGemmMinStates && m.B >= kDenseGemmMinBatch;
+  if (dense_gemm_mfma_ok(m.S)) return m.B >= 16 || (m.S >= 4096 && m.B >= 4);
+  return m.S >= 4096 && m.B >= 32;
 }
 
 // one rocBLAS handle per host thread and device (handles are not thread safe)
@@ -1258,8 +1262,12 @@ static int dense_backward(const Model& m, const double* reward, const uint8_t* t
   dense_bwd_init_launch(d, terminal, w, st);
   const long long collapsed = 2LL * m.S - 1;
   const bool gemm = dense_gemm(m);
+  // GEMM engine: the hand-written fp64 MFMA kernel (dense.hip dense_gemm_kernel), or
+  // the library dgemm (IRLMX_DENSE_GEMM_ENGINE=rocblas; also for S % 4 != 0)
+  const char* eng = getenv("IRLMX_DENSE_GEMM_ENGINE");
+  const bool lib = (eng && strcmp(eng, "rocblas") == 0) || !dense_gemm_mfma_ok(m.S);
   rocblas_handle h = nullptr;
-  if (gemm)
+  if (gemm && lib)
     if (int rc = rocblas_for(st, &h)) return rc;
   const double one = 1.0, zero = 0.0;
   int r3 = 0;
@@ -1267,8 +1275,10 @@ static int dense_backward(const Model& m, const double* reward, const uint8_t* t
     if (gemm) {
       // column-major view: C [S x B] = op(M) . ZS with M row-major = (M^T col-major), op = transpose
       const double* zin = (it & 1) ? ws.buf1 : ws.buf0;
-      if (rocblas_dgemm(h, rocblas_operation_transpose, rocblas_operation_none, m.S, m.B, m.S, &one, m.col_val, m.S,
-                        zin, m.S, &zero, ws.wgt, m.S) != rocblas_status_success) {
+      if (!lib) {
+        dense_gemm_launch(m.col_val, zin, ws.wgt, m.S, m.B, st);
+      } else if (rocblas_dgemm(h, rocblas_operation_transpose, rocblas_operation_none, m.S, m.B, m.S, &one,
+                               m.col_val, m.S, zin, m.S, &zero, ws.wgt, m.S) != rocblas_status_success) {
         set_error("rocblas_dgemm failed");
         return IRLMX_EHIP;
       }

@@ -116,8 +116,9 @@ def test_random_dense_2048_vs_dense_oracle(dev, dense2048):
 
 
 def test_shared_table_gemm_backward(dev, dense2048, monkeypatch):
-    """One dense table, 16 reward vectors: the backward sweep as one dgemm over all
-    instances (plan "dense-gemm", forced: at S = 2048 streaming is faster) equals the
+    """One dense table, 16 reward vectors: the backward sweep as one GEMM over all
+    instances (plan "dense-gemm") -- on the
+    hand-written fp64 MFMA kernel and on the library dgemm -- equals the
     per-instance streaming kernel and the oracle (instance 0 carries the
     fixture's reward)."""
     from irlmx import DeviceMDP, ops
@@ -127,10 +128,12 @@ def test_shared_table_gemm_backward(dev, dense2048, monkeypatch):
     rew = np.random.default_rng(16).uniform(0.0, 1.0, (B, P.shape[0]))
     rew[0] = r
     tm = ops.terminal_mask(term, P.shape[0], batch=B, device=dev)
-    assert ops.execution_plan(mdp, "backward")["shape"] == "dense"   # below the measured crossover
-    monkeypatch.setenv("IRLMX_DENSE_GEMM_MIN", "2")
-    assert ops.execution_plan(mdp, "backward")["shape"] == "dense-gemm"
-    pi_gemm = ops.backward_maxent(mdp, rew, tm).cpu().numpy()
+    assert ops.execution_plan(mdp, "backward")["shape"] == "dense-gemm"   # 16 instances: the MFMA kernel
+    pi_gemm = ops.backward_maxent(mdp, rew, tm).cpu().numpy()            # hand-written fp64 MFMA kernel
+    monkeypatch.setenv("IRLMX_DENSE_GEMM_ENGINE", "rocblas")
+    pi_lib = ops.backward_maxent(mdp, rew, tm).cpu().numpy()             # library dgemm
+    monkeypatch.delenv("IRLMX_DENSE_GEMM_ENGINE")
+    close(pi_gemm, pi_lib, 1e-12, "mfma kernel vs rocblas")
     monkeypatch.setenv("IRLMX_DENSE_GEMM_MIN", "1000000")
     assert ops.execution_plan(mdp, "backward")["shape"] == "dense"
     pi_stream = ops.backward_maxent(mdp, rew, tm).cpu().numpy()
@@ -146,3 +149,21 @@ def test_dropin_accepts_dense_tables(dev, dense2048):
     P, r, term, p0, z = dense2048
     close(M.local_action_probabilities(P, term, r), z["pi"], 1e-9, "drop-in pi")
     close(S.value_iteration(P, r, 0.9), z["v"], 1e-12, "drop-in v")
+
+
+@pytest.mark.parametrize("n,batch", [(300, 5), (301, 3), (1040, 37)])
+def test_gemm_edges(dev, monkeypatch, n, batch):
+    """The MFMA kernel's partial row / instance tiles (S not a multiple of 32, B not
+    a multiple of 16) and the library fallback (S % 4 != 0) against the streaming
+    kernel, forced onto the GEMM plan."""
+    from irlmx import DeviceMDP, ops
+    P, _, _, _ = O.random_dense_mdp(n, 3, seed=n)
+    mdp = DeviceMDP.from_dense(P, device=dev, layout="dense").with_batch(batch)
+    rew = np.random.default_rng(n).uniform(0.0, 1.0, (batch, n))
+    tm = ops.terminal_mask([n - 1], n, batch=batch, device=dev)
+    monkeypatch.setenv("IRLMX_DENSE_GEMM_MIN", "2")
+    assert ops.execution_plan(mdp, "backward")["shape"] == "dense-gemm"
+    pi_gemm = ops.backward_maxent(mdp, rew, tm).cpu().numpy()
+    monkeypatch.setenv("IRLMX_DENSE_GEMM_MIN", "1000000")
+    pi_stream = ops.backward_maxent(mdp, rew, tm).cpu().numpy()
+    close(pi_gemm, pi_stream, 1e-12, f"gemm vs streaming S={n} B={batch}")

@@ -17,15 +17,16 @@ for S in sizes:
     P /= P.sum(axis=1, keepdims=True)
     one = DeviceMDP.from_dense(P, device=dev)
     del P
-    for B in (1, 4, 16, 64):
+    for B in [int(x) for x in os.environ.get("BATCHES", "1,4,16,64").split(",")]:
         mdp = one.with_batch(B)
         r = rng.uniform(0.0, 1.0, (B, S))
         tm = ops.terminal_mask([S - 1], S, batch=B, device=dev)
         res = {}
-        for mode, env in (("stream", "1000000"), ("gemm", "1")):
-            if B == 1 and mode == "gemm":
+        for mode, env, eng in (("stream", "1000000", "mfma"), ("gemm-mfma", "1", "mfma"), ("gemm-rocblas", "1", "rocblas")):
+            if B == 1 and mode != "stream":
                 continue
             os.environ["IRLMX_DENSE_GEMM_MIN"] = env
+            os.environ["IRLMX_DENSE_GEMM_ENGINE"] = eng
             ops.backward_maxent(mdp, r, tm); torch.cuda.synchronize()
             t = time.perf_counter(); pi = ops.backward_maxent(mdp, r, tm); torch.cuda.synchronize()
             dt = time.perf_counter() - t
@@ -34,7 +35,8 @@ for S in sizes:
                   f"{B * S * S * 8 * 2 * S / dt / 1e9 if mode == 'stream' else S * S * 8 * 2 * S / dt / 1e9:.0f} GB/s "
                   f"matrix stream, {2.0 * S * S * B * 2 * S / dt / 1e12:.2f} TFLOP/s", flush=True)
         os.environ.pop("IRLMX_DENSE_GEMM_MIN", None)
-        if B in (1, 16):
+        os.environ.pop("IRLMX_DENSE_GEMM_ENGINE", None)
+        if B in (1, 16) and not os.environ.get("BACKWARD_ONLY"):
             pi = ops.backward_maxent(mdp, r, tm)
             p0 = np.zeros((B, S)); p0[:, 0] = 1.0
             torch.cuda.synchronize(); t = time.perf_counter()
