@@ -66,8 +66,11 @@ void dense_bwd_final_launch(const DenseView& d, const double* reward, int rescal
 void dense_bellman_sweep_launch(const DenseView& d, const DenseBellman& a, DenseBufs w, long long it, int r3,
                                 hipStream_t st);
 void dense_bellman_finish_launch(const DenseView& d, const DenseBellman& a, DenseBufs w, hipStream_t st);
-// C[b][s] = sum_t M[s][t] Z[b][t] on the fp64 matrix cores (needs S % 4 == 0)
+// shared table: the sweep's A products P_a . [v_1 .. v_B] on the MFMA kernel (w.wt = [B][A][S]) + the update
+void dense_bellman_gemm_sweep_launch(const DenseView& d, const DenseBellman& a, DenseBufs w, long long it, int r3,
+                                     hipStream_t st);
+// C[b][r] = sum_t M[r][t] Z[b][t], M [R][S], Z [B][S], on the fp64 matrix cores (needs S % 4 == 0)
 bool dense_gemm_mfma_ok(int S);
-void dense_gemm_launch(const double* M, const double* Z, double* C, int S, int B, hipStream_t st);
+void dense_gemm_launch(const double* M, const double* Z, double* C, int R, int S, int B, hipStream_t st);
 
 }  // namespace irlmx

@@ -355,6 +355,35 @@ dense_bellman_sweep_kernel(DenseView d, DenseBellman a, DenseBufs w, long long i
   if (blockIdx.x == 0 && threadIdx.x == 0) w.slots[b * 3 + (r3 == 2 ? 0 : r3 + 1)] = 0ull;
 }
 
+// One Bellman sweep of all instances of a shared table from GEMM products:
+// c[b][a * S + s] = (P_a v_b)[s], one MFMA GEMM over the stacked P_a; the
+// rest of dense_bellman_sweep_kernel's update and bookkeeping, thread per state.
+__global__ void __launch_bounds__(kDenseThreads)
+dense_bellman_gemm_epilogue_kernel(DenseView d, DenseBellman a, DenseBufs w, const double* __restrict__ c,
+                                   long long it, int r3) {
+  const int b = blockIdx.y, S = d.S, A = d.A;
+  const int s = blockIdx.x * blockDim.x + threadIdx.x;
+  if (dense_should_stop(b, it, r3, a.eps, a.max_iter, w, a.status)) return;
+  const double* vin = ((it & 1) ? w.buf1 : w.buf0) + (size_t)b * S;
+  double* vout = ((it & 1) ? w.buf0 : w.buf1) + (size_t)b * S;
+  unsigned long long mx = 0ull;
+  if (s < S) {
+    double dots[kDenseMaxActions];
+#pragma unroll
+    for (int act = 0; act < kDenseMaxActions; ++act)
+      dots[act] = act < A ? c[((size_t)b * A + act) * S + s] : 0.0;
+    const double nv = dense_backup(a, A, dots, a.reward[(size_t)b * S + s], a.soft ? a.phi[(size_t)b * S + s] : 0.0);
+    vout[s] = nv;
+    mx = abs_bits(nv - vin[s]);
+  }
+  for (int off = 32; off > 0; off >>= 1) {
+    const unsigned long long o = __shfl_xor(mx, off, kWave);
+    mx = o > mx ? o : mx;
+  }
+  block_max_slot(mx, &w.slots[b * 3 + r3]);
+  if (blockIdx.x == 0 && threadIdx.x == 0) w.slots[b * 3 + (r3 == 2 ? 0 : r3 + 1)] = 0ull;
+}
+
 // value out; soft VI: pi = exp(q - v) with q from the last sweep's input (maxent.py:341)
 template <bool LDSV>
 __global__ void __launch_bounds__(kDenseThreads)
@@ -406,7 +435,8 @@ typedef double f64x4 __attribute__((ext_vector_type(4)));
 // S and B so that the grid fills the chip)
 template <int ST, int NBT>
 __global__ void __launch_bounds__(kGemmWaves * kWave)
-dense_gemm_kernel(const double* __restrict__ M, const double* __restrict__ Z, double* __restrict__ C, int S, int B) {
+dense_gemm_kernel(const double* __restrict__ M, const double* __restrict__ Z, double* __restrict__ C, int R, int S,
+                  int B) {  // M [R][S], Z [B][S] -> C [B][R]
   extern __shared__ __attribute__((aligned(16))) double part[];  // [waves][ST][NBT][4][64]
   const int wave = threadIdx.x / kWave, l = threadIdx.x & (kWave - 1);
   const int s0 = blockIdx.x * 16 * ST, b0 = blockIdx.y * 16 * NBT;
@@ -425,7 +455,7 @@ dense_gemm_kernel(const double* __restrict__ M, const double* __restrict__ Z, do
 #pragma unroll
   for (int st = 0; st < ST; ++st) {
     const int r = s0 + 16 * st + i;
-    mok[st] = r < S;
+    mok[st] = r < R;
     mrow[st] = M + (size_t)(mok[st] ? r : 0) * S;
   }
 #pragma unroll
@@ -488,7 +518,7 @@ dense_gemm_kernel(const double* __restrict__ M, const double* __restrict__ Z, do
     for (int w = 1; w < kGemmWaves; ++w) v += part[(size_t)w * kOut + e];
     const int ll = e % kWave, r = (e / kWave) % 4, bt = (e / (kWave * 4)) % NBT, st = e / (kWave * 4 * NBT);
     const int row = s0 + 16 * st + (ll >> 4) + 4 * r, col = b0 + 16 * bt + (ll & 15);
-    if (row < S && col < B) C[(size_t)col * S + row] = v;
+    if (row < R && col < B) C[(size_t)col * R + row] = v;
   }
 }
 
@@ -565,6 +595,15 @@ void dense_bellman_sweep_launch(const DenseView& d, const DenseBellman& a, Dense
     hipLaunchKernelGGL(dense_bellman_sweep_kernel<false>, row_grid(d), dim3(kDenseThreads), 0, st, d, a, w, it, r3);
 }
 
+void dense_bellman_gemm_sweep_launch(const DenseView& d, const DenseBellman& a, DenseBufs w, long long it, int r3,
+                                     hipStream_t st) {
+  const double* vin = (it & 1) ? w.buf1 : w.buf0;
+  // all actions in one GEMM: the stacked P [A * S][S] times [v_1 .. v_B] -> c[b][a * S + s]
+  dense_gemm_launch(d.P, vin, w.wt, d.A * d.S, d.S, d.B, st);
+  hipLaunchKernelGGL(dense_bellman_gemm_epilogue_kernel, dim3((d.S + kDenseThreads - 1) / kDenseThreads, d.B),
+                     dim3(kDenseThreads), 0, st, d, a, w, w.wt, it, r3);
+}
+
 void dense_bellman_finish_launch(const DenseView& d, const DenseBellman& a, DenseBufs w, hipStream_t st) {
   if (lds_vec(d.S))
     hipLaunchKernelGGL(dense_bellman_finish_kernel<true>, row_grid(d), dim3(kDenseThreads), lds_bytes(d.S), st, d, a,
@@ -580,27 +619,27 @@ namespace irlmx {
 bool dense_gemm_mfma_ok(int S) { return S % 4 == 0; }
 
 template <int ST, int NBT>
-static void gemm_go(const double* M, const double* Z, double* C, int S, int B, hipStream_t st) {
+static void gemm_go(const double* M, const double* Z, double* C, int R, int S, int B, hipStream_t st) {
   const size_t lds = (size_t)kGemmWaves * ST * NBT * 4 * kWave * sizeof(double);
   (void)hipFuncSetAttribute((const void*)&dense_gemm_kernel<ST, NBT>, hipFuncAttributeMaxDynamicSharedMemorySize,
                             (int)lds);
-  const dim3 grid((S + 16 * ST - 1) / (16 * ST), (B + 16 * NBT - 1) / (16 * NBT));
-  hipLaunchKernelGGL((dense_gemm_kernel<ST, NBT>), grid, dim3(kGemmWaves * kWave), lds, st, M, Z, C, S, B);
+  const dim3 grid((R + 16 * ST - 1) / (16 * ST), (B + 16 * NBT - 1) / (16 * NBT));
+  hipLaunchKernelGGL((dense_gemm_kernel<ST, NBT>), grid, dim3(kGemmWaves * kWave), lds, st, M, Z, C, R, S, B);
 }
 
-void dense_gemm_launch(const double* M, const double* Z, double* C, int S, int B, hipStream_t st) {
+void dense_gemm_launch(const double* M, const double* Z, double* C, int R, int S, int B, hipStream_t st) {
   const int nbt = B <= 16 ? 1 : (B <= 32 ? 2 : 4);
   const int ny = (B + 16 * nbt - 1) / (16 * nbt);
   // two row tiles per wave (half the Z re-reads) while that still gives >= 256 workgroups
-  const bool st2 = (long long)((S + 31) / 32) * ny >= 256;
+  const bool st2 = (long long)((R + 31) / 32) * ny >= 256;
   if (st2) {
-    if (nbt == 1) gemm_go<2, 1>(M, Z, C, S, B, st);
-    else if (nbt == 2) gemm_go<2, 2>(M, Z, C, S, B, st);
-    else gemm_go<2, 4>(M, Z, C, S, B, st);
+    if (nbt == 1) gemm_go<2, 1>(M, Z, C, R, S, B, st);
+    else if (nbt == 2) gemm_go<2, 2>(M, Z, C, R, S, B, st);
+    else gemm_go<2, 4>(M, Z, C, R, S, B, st);
   } else {
-    if (nbt == 1) gemm_go<1, 1>(M, Z, C, S, B, st);
-    else if (nbt == 2) gemm_go<1, 2>(M, Z, C, S, B, st);
-    else gemm_go<1, 4>(M, Z, C, S, B, st);
+    if (nbt == 1) gemm_go<1, 1>(M, Z, C, R, S, B, st);
+    else if (nbt == 2) gemm_go<1, 2>(M, Z, C, R, S, B, st);
+    else gemm_go<1, 4>(M, Z, C, R, S, B, st);
   }
 }
 

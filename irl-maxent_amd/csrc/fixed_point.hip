@@ -156,6 +156,8 @@ static Ws carve(const Model& m, int op, void* base) {
   size_t nw = 0;
   if (op == IRLMX_OP_FORWARD) nw = B * m.Kc * S;  // dense: the per-instance gather matrices WT [B][S][S]
   if (op == IRLMX_OP_BACKWARD) nw = m.dense ? B * S : B * m.K * S;  // reward-folded; dense: the GEMM product
+  if ((op == IRLMX_OP_SOFT_BACKWARD || op == IRLMX_OP_VALUE_ITERATION) && m.dense && m.shared)
+    nw = (size_t)m.A * B * S;  // the per-action GEMM products of a shared dense table
   w.wgt = (double*)take(nw * sizeof(double));
   w.bad = (int32_t*)take(B * sizeof(int32_t));
   const bool sweep = !use_fused(m, op);
@@ -1276,7 +1278,7 @@ static int dense_backward(const Model& m, const double* reward, const uint8_t* t
       // column-major view: C [S x B] = op(M) . ZS with M row-major = (M^T col-major), op = transpose
       const double* zin = (it & 1) ? ws.buf1 : ws.buf0;
       if (!lib) {
-        dense_gemm_launch(m.col_val, zin, ws.wgt, m.S, m.B, st);
+        dense_gemm_launch(m.col_val, zin, ws.wgt, m.S, m.S, m.B, st);
       } else if (rocblas_dgemm(h, rocblas_operation_transpose, rocblas_operation_none, m.S, m.B, m.S, &one,
                                m.col_val, m.S, zin, m.S, &zero, ws.wgt, m.S) != rocblas_status_success) {
         set_error("rocblas_dgemm failed");
@@ -1349,7 +1351,9 @@ extern "C" int irlmx_execution_plan(const irlmx_mdp* mdp, int32_t op, int64_t* p
     return 0;
   }
   if (m.dense) {
-    plan[0] = (op == IRLMX_OP_BACKWARD && dense_gemm(m)) ? IRLMX_SHAPE_DENSE_GEMM : IRLMX_SHAPE_DENSE;
+    const bool gemm = op == IRLMX_OP_BACKWARD ? dense_gemm(m)
+                      : (op != IRLMX_OP_FORWARD && dense_gemm(m) && dense_gemm_mfma_ok(m.S));
+    plan[0] = gemm ? IRLMX_SHAPE_DENSE_GEMM : IRLMX_SHAPE_DENSE;
     plan[7] = kDenseThreads;
     plan[9] = m.S <= kDenseLdsMaxStates ? (int64_t)m.S * 8 : 0;
     return 0;
@@ -1499,7 +1503,11 @@ static int bellman_common(const irlmx_mdp* mdp, const double* reward, const doub
     const DenseBufs w = dense_bufs(ws);
     const DenseBellman db{reward, phi, discount, eps, (long long)max_iter, average, soft ? 1 : 0, p_action, value,
                           iterations, status};
-    int rc = run_until_done(ws, m.B, st, [&](long long it, int r3) { dense_bellman_sweep_launch(d, db, w, it, r3, st); });
+    const bool gemm = dense_gemm(m) && dense_gemm_mfma_ok(m.S);  // the P . [v_1 .. v_B] products on the MFMA kernel
+    int rc = run_until_done(ws, m.B, st, [&](long long it, int r3) {
+      if (gemm) dense_bellman_gemm_sweep_launch(d, db, w, it, r3, st);
+      else dense_bellman_sweep_launch(d, db, w, it, r3, st);
+    });
     if (rc) return rc;
     dense_bellman_finish_launch(d, db, w, st);
     e = hipGetLastError();

@@ -167,3 +167,35 @@ def test_gemm_edges(dev, monkeypatch, n, batch):
     monkeypatch.setenv("IRLMX_DENSE_GEMM_MIN", "1000000")
     pi_stream = ops.backward_maxent(mdp, rew, tm).cpu().numpy()
     close(pi_gemm, pi_stream, 1e-12, f"gemm vs streaming S={n} B={batch}")
+
+
+def test_shared_table_gemm_soft_vi_and_vi(dev, dense2048, monkeypatch):
+    """Soft VI (maxent.py:326-338) and VI (solver.py:40-50) of 16 reward vectors on one
+    dense table: every sweep's P_a . [v_1 .. v_16] on the fp64 MFMA kernel (plan
+    "dense-gemm"), against the per-instance streaming kernel (sweep counts
+    identical, values within 1e-12) and the dense oracle (instance 0)."""
+    from irlmx import DeviceMDP, ops
+    from irlmx.batch import terminal_reward
+    P, r, term, p0, z = dense2048
+    n, B = P.shape[0], 16
+    mdp = DeviceMDP.from_dense(P, device=dev).with_batch(B)
+    rew = np.random.default_rng(161).uniform(0.0, 1.0, (B, n))
+    rew[0] = r
+    phi = terminal_reward(term, n, B, dev)
+    assert ops.execution_plan(mdp, "soft_backward")["shape"] == "dense-gemm"
+
+    def run():
+        cpi, cv, ks, _ = ops.soft_backward(mdp, rew, phi, 0.7)
+        v, kv, _ = ops.value_iteration(mdp, rew, 0.9)
+        return cpi.cpu().numpy(), cv.cpu().numpy(), ks.cpu().numpy(), v.cpu().numpy(), kv.cpu().numpy()
+
+    g = run()
+    monkeypatch.setenv("IRLMX_DENSE_GEMM_MIN", "1000000")
+    assert ops.execution_plan(mdp, "soft_backward")["shape"] == "dense"
+    s = run()
+    assert np.array_equal(g[2], s[2]) and np.array_equal(g[4], s[4])
+    for i in (0, 1, 3):
+        close(g[i], s[i], 1e-12, f"gemm vs streaming {i}")
+    assert int(g[2][0]) == int(z["k_s"]) and int(g[4][0]) == int(z["k_v"])
+    close(g[0][0], z["cpi"], 1e-9, "soft pi vs oracle")
+    close(g[3][0], z["v"], 1e-12, "v vs oracle")
