@@ -169,7 +169,7 @@ static Ws carve(const Model& m, int op, void* base) {
   w.ndone = (int32_t*)take(sizeof(int32_t) * 4);
   const bool cl = sweep && m.stencil && (op == IRLMX_OP_FORWARD || op == IRLMX_OP_BACKWARD);
   GridPlan gp{0, 0, 0};
-  const bool gr = sweep && (op == IRLMX_OP_SOFT_BACKWARD || op == IRLMX_OP_VALUE_ITERATION) && grid_plan(m, op, &gp);
+  const bool gr = sweep && grid_plan(m, op, &gp);
   // cluster halo exchange: [B][2][S] and [B][3][H] 16-byte granule pairs;
   // grid shape: [B][3][S] value and [B][3][bpi] block-delta granules
   w.gran = (unsigned long long*)take(cl ? 2 * B * S * 16 : (gr ? 3 * B * S * 16 : 0));
@@ -991,6 +991,233 @@ __global__ void __launch_bounds__(kGridThreads) bellman_grid_kernel(SoftArgs a, 
   }
 }
 
+// The grid shape for the linear loops of ELL models (generic sparsity, S > 4096):
+// the forward (MODE kModeFwd: d <- p0 + sum_k w[k] d[src_k], until max|dd| <= eps;
+// fwd_sweep_kernel's arithmetic) and the backward (kModeBwd: 2S - 1 collapsed
+// sweeps zs <- ldexp(sum_k w[k] zs[nbr_k], e), e from the previous sweep's
+// maximum, then the per-action sweep; bwd_sweep_kernel / bwd_final_kernel's
+// arithmetic).  Same exchange as bellman_grid_kernel; the block maxima carry
+// max|dd| (forward) or max|zs| (backward: the rescale exponent, and a NaN /
+// inf there is bwd_nonfinite_rule's flag -- ordered bits sort them above every
+// finite value).
+struct LinearGridArgs {
+  Model m;
+  const double* w;      // [B][K][S] forward gather weights / reward-folded backward weights
+  const double* vin;    // forward: p0 [B][S]; backward: reward [B][S]
+  const uint8_t* term;  // backward: terminal mask
+  const int32_t* bad;   // [B] non-finite policy (forward) / weights (backward)
+  double eps;
+  long long max_iter;
+  int rescale;
+  double* out;          // forward: svf [B][S]; backward: pi [B][S][A]
+  int64_t* iters;
+  int32_t* status;
+};
+
+template <int MODE, int SPT, int KMAX>
+__global__ void __launch_bounds__(kGridThreads) linear_grid_kernel(LinearGridArgs a, GridArgs g) {
+  const Model& m = a.m;
+  const int S = m.S;
+  const int Kr = MODE == kModeFwd ? m.Kc : m.K;
+  int lin = blockIdx.x;
+  if (g.xcd_group) {
+    const int grp = blockIdx.x % 8, kk = blockIdx.x / 8;
+    const int il = grp + 8 * (kk / g.bpi);
+    if (il >= g.nb) return;
+    lin = il * g.bpi + kk % g.bpi;
+  }
+  const int b = lin / g.bpi, blk = lin % g.bpi, tid = threadIdx.x;
+  constexpr int K = KMAX;
+  __shared__ unsigned long long red_in[kGridThreads / kWave], red_out[kGridThreads / kWave];
+  __shared__ int lflag;
+  int sidx[SPT];
+  bool ok[SPT];
+  int nb[SPT][K];
+  double w[SPT][K], c0[SPT], cur[SPT];
+  if (MODE == kModeFwd && a.bad[b]) {  // non-finite policy: the reference's dense product is NaN after one sweep
+#pragma unroll
+    for (int j = 0; j < SPT; ++j) {
+      const int s = (blk * SPT + j) * kGridThreads + tid;
+      if (s < S) a.out[(size_t)b * S + s] = kNaN;
+    }
+    if (blk == 0 && tid == 0) { a.iters[b] = 1; a.status[b] = IRLMX_NONFINITE; }
+    return;
+  }
+#pragma unroll
+  for (int j = 0; j < SPT; ++j) {
+    const int s = (blk * SPT + j) * kGridThreads + tid;
+    sidx[j] = s;
+    ok[j] = s < S;
+    const int ss = ok[j] ? s : 0;
+    c0[j] = MODE == kModeFwd ? a.vin[(size_t)b * S + ss] : 0.0;
+    cur[j] = MODE == kModeBwd ? (a.term[(size_t)b * S + ss] ? 1.0 : 0.0) : 0.0;  // maxent.py:146-147 / d = 0
+#pragma unroll
+    for (int k = 0; k < K; ++k) {
+      nb[j][k] = k < Kr ? (MODE == kModeFwd ? col_src(m, b, ss, k) : row_nbr(m, b, ss, k)) : ss;
+      w[j][k] = k < Kr ? a.w[((size_t)b * Kr + k) * S + ss] : 0.0;
+    }
+  }
+  if (tid == 0) lflag = 0;
+  const __amdgpu_buffer_rsrc_t rg = gran_rsrc(g.gran + (size_t)b * 6 * S, 48u * (unsigned)S);
+  const __amdgpu_buffer_rsrc_t rd = gran_rsrc(g.dgran + (size_t)b * 8 * g.bpi, 64u * (unsigned)g.bpi);
+  const unsigned salt = (g.salt & 0xFFFu) << 20;
+  bool plain = false;
+  {  // XCC ids (bellman_grid_kernel)
+    unsigned xcc;
+    asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
+    xcc &= 0xFu;
+    const unsigned htag = salt | 0xFFFFFu;
+    if (tid == 0) gran_store(rd, (3u * (unsigned)g.bpi + (unsigned)blk) * 16u, xcc, htag, false);
+    unsigned off[1] = {(3u * (unsigned)g.bpi + (unsigned)tid) * 16u};
+    unsigned long long v[1] = {xcc};
+    if (!gran_gather<1>(rd, rd, off, tid < g.bpi ? 1u : 0u, htag, v)) lflag = 1;
+    const unsigned long long diff = wave_or_u64(tid < g.bpi ? (v[0] ^ xcc) : 0ull);
+    if ((tid & (kWave - 1)) == 0) red_in[tid / kWave] = diff;
+    __syncthreads();
+    if (lflag) {
+      if (tid == 0) atomicOr(g.err, 1);
+      return;
+    }
+    unsigned long long any = 0ull;
+#pragma unroll
+    for (int i = 0; i < kGridThreads / kWave; ++i) any |= red_in[i];
+    plain = g.xcd_group && any == 0ull;
+    __syncthreads();
+  }
+  // backward: publish the start vector as sweep 0 (its neighbours read it)
+  const long long total = MODE == kModeBwd ? 2LL * S - 1 : -1;
+  double delta = 0.0;
+  unsigned long long gmax = 0ull;  // backward: max |zs| of the vector the next sweep reads
+  bool nonfinite = false;
+  long long k = 0;
+  if (MODE == kModeBwd) {
+    const unsigned tag0 = salt | 1u;  // tag of sweep k: salt | (k + 1), never 0 (a zeroed workspace)
+    unsigned long long dm = 0ull;
+#pragma unroll
+    for (int j = 0; j < SPT; ++j)
+      if (ok[j]) {
+        gran_store(rg, (unsigned)sidx[j] * 16u, dbits(cur[j]), tag0, plain);
+        const unsigned long long d = abs_bits(cur[j]);
+        dm = d > dm ? d : dm;
+      }
+    dm = wave_max_u64(dm);
+    if ((tid & (kWave - 1)) == 0) red_out[tid / kWave] = dm;
+    __syncthreads();
+    if (tid == 0) {
+      unsigned long long mx = 0ull;
+      for (int i = 0; i < kGridThreads / kWave; ++i) mx = red_out[i] > mx ? red_out[i] : mx;
+      gran_store(rd, (unsigned)blk * 16u, mx, tag0, plain);
+    }
+  }
+  double nv[SPT][K];  // the neighbours' values of the vector the next sweep reads
+  for (;;) {
+    if (MODE == kModeFwd && k == 0) {
+#pragma unroll
+      for (int j = 0; j < SPT; ++j)
+#pragma unroll
+        for (int kk = 0; kk < K; ++kk) nv[j][kk] = 0.0;
+    } else {
+      const unsigned tag = salt | ((unsigned)(k + 1) & 0xFFFFFu);
+      const unsigned slot = (unsigned)(k % 3);
+      unsigned off[SPT * K + 1];
+      unsigned want = 0;
+#pragma unroll
+      for (int j = 0; j < SPT; ++j)
+#pragma unroll
+        for (int kk = 0; kk < K; ++kk) {
+          off[j * K + kk] = (slot * (unsigned)S + (unsigned)nb[j][kk]) * 16u;
+          want |= (ok[j] && kk < Kr ? 1u : 0u) << (j * K + kk);
+        }
+      off[SPT * K] = (slot * (unsigned)g.bpi + (unsigned)tid) * 16u;
+      want |= (tid < g.bpi ? 1u : 0u) << (SPT * K);
+      unsigned long long v[SPT * K + 1];
+      if (!gran_gather<SPT * K + 1>(rg, rd, off, want, tag, v)) lflag = 1;
+#pragma unroll
+      for (int j = 0; j < SPT; ++j)
+#pragma unroll
+        for (int kk = 0; kk < K; ++kk) nv[j][kk] = (ok[j] && kk < Kr) ? bits_double(v[j * K + kk]) : 0.0;
+      unsigned long long d = tid < g.bpi ? v[SPT * K] : 0ull;
+      d = wave_max_u64(d);
+      if ((tid & (kWave - 1)) == 0) red_in[tid / kWave] = d;
+      __syncthreads();
+      if (lflag) {
+        if (tid == 0) atomicOr(g.err, 1);
+        return;
+      }
+      unsigned long long mx = 0ull;
+#pragma unroll
+      for (int i = 0; i < kGridThreads / kWave; ++i) mx = red_in[i] > mx ? red_in[i] : mx;
+      if (MODE == kModeFwd) {
+        delta = bits_double(mx);
+        if (!(delta > a.eps) || (a.max_iter > 0 && k >= a.max_iter)) break;  // maxent.py:108
+      } else {
+        gmax = mx;
+        nonfinite |= mx >= 0x7FF0000000000000ull;  // some |zs| is inf or NaN
+        if (k >= total) break;  // neighbours of zs_{2S-1} gathered: the per-action sweep
+      }
+    }
+    const int e = (MODE == kModeBwd && a.rescale && k > 0) ? rescale_exponent(bits_double(gmax)) : 0;
+    unsigned long long dmax = 0ull;
+    const unsigned tag1 = salt | ((unsigned)(k + 2) & 0xFFFFFu);
+    const unsigned slot1 = (unsigned)((k + 1) % 3);
+#pragma unroll
+    for (int j = 0; j < SPT; ++j) {
+      double acc = 0.0;
+#pragma unroll
+      for (int kk = 0; kk < K; ++kk)
+        if (kk < Kr) acc = fma(w[j][kk], nv[j][kk], acc);
+      const double v = MODE == kModeFwd ? c0[j] + acc : ldexp(acc, e);
+      if (ok[j]) {
+        const unsigned long long d = MODE == kModeFwd ? abs_bits(v - cur[j]) : abs_bits(v);
+        dmax = d > dmax ? d : dmax;
+        gran_store(rg, (slot1 * (unsigned)S + (unsigned)sidx[j]) * 16u, dbits(v), tag1, plain);
+      }
+      cur[j] = v;
+    }
+    dmax = wave_max_u64(dmax);
+    if ((tid & (kWave - 1)) == 0) red_out[tid / kWave] = dmax;
+    __syncthreads();
+    if (tid == 0) {
+      unsigned long long mx = 0ull;
+      for (int i = 0; i < kGridThreads / kWave; ++i) mx = red_out[i] > mx ? red_out[i] : mx;
+      gran_store(rd, (slot1 * (unsigned)g.bpi + (unsigned)blk) * 16u, mx, tag1, plain);
+    }
+    ++k;
+  }
+  if (MODE == kModeFwd) {
+#pragma unroll
+    for (int j = 0; j < SPT; ++j)
+      if (ok[j]) a.out[(size_t)b * S + sidx[j]] = cur[j];
+    if (blk == 0 && tid == 0) { a.iters[b] = k; a.status[b] = finish_status(delta, a.eps); }
+  } else {
+    // the last of the 2*S sweeps, per action (bwd_final_kernel's arithmetic)
+    const int A = m.A;
+    const int e = a.rescale ? rescale_exponent(bits_double(gmax)) : 0;
+    const bool all_nan = nonfinite || a.bad[b];
+#pragma unroll
+    for (int j = 0; j < SPT; ++j) {
+      if (!ok[j]) continue;
+      const int s = sidx[j];
+      double* pr = a.out + ((size_t)b * S + s) * A;
+      if (all_nan) {
+        for (int act = 0; act < A; ++act) pr[act] = kNaN;
+        continue;
+      }
+      const double er = exp(a.vin[(size_t)b * S + s]);
+      double za[kMaxActions];
+      double zsum = 0.0;
+      for (int act = 0; act < A; ++act) {
+        double acc = 0.0;
+        for (int kk = 0; kk < Kr; ++kk) acc = fma(row_val(m, b, act, kk, s), nv[j][kk], acc);
+        za[act] = ldexp(__dmul_rn(er, acc), e);
+        zsum = __dadd_rn(zsum, za[act]);
+      }
+      for (int act = 0; act < A; ++act) pr[act] = za[act] / zsum;
+    }
+    if (blk == 0 && tid == 0) a.status[b] = IRLMX_OK;
+  }
+}
+
 template <bool SOFT>
 static void* bellman_grid_fn(int spt, int kmax) {
   if (kmax == 5) {
@@ -1008,6 +1235,34 @@ static void* bellman_grid_fn(int spt, int kmax) {
   return nullptr;
 }
 static int grid_kmax(const Model& m) { return m.K <= 5 ? 5 : (m.K <= 8 ? 8 : 0); }
+static int grid_kmax_fwd(const Model& m) { return m.Kc <= 5 ? 5 : (m.Kc <= 8 ? 8 : 0); }
+
+template <int MODE>
+static void* linear_grid_fn(int spt, int kmax) {
+  if (kmax == 5) {
+    switch (spt) {
+      case 1: return (void*)&linear_grid_kernel<MODE, 1, 5>;
+      case 2: return (void*)&linear_grid_kernel<MODE, 2, 5>;
+      case 4: return (void*)&linear_grid_kernel<MODE, 4, 5>;
+    }
+  } else if (kmax == 8) {
+    switch (spt) {
+      case 1: return (void*)&linear_grid_kernel<MODE, 1, 8>;
+      case 2: return (void*)&linear_grid_kernel<MODE, 2, 8>;
+    }
+  }
+  return nullptr;
+}
+
+static void* grid_fn(const Model& m, int op, int spt) {
+  switch (op) {
+    case IRLMX_OP_SOFT_BACKWARD: return bellman_grid_fn<true>(spt, grid_kmax(m));
+    case IRLMX_OP_VALUE_ITERATION: return bellman_grid_fn<false>(spt, grid_kmax(m));
+    case IRLMX_OP_FORWARD: return linear_grid_fn<kModeFwd>(spt, grid_kmax_fwd(m));
+    case IRLMX_OP_BACKWARD: return linear_grid_fn<kModeBwd>(spt, grid_kmax(m));
+  }
+  return nullptr;
+}
 
 static int grid_capacity(void* fn) {
   int dev = 0, cus = 0, per_cu = 0;
@@ -1020,12 +1275,18 @@ static int grid_capacity(void* fn) {
 // the smallest states-per-thread whose grid is co-resident (all workgroups must
 // run at once: they wait on each other's granules); IRLMX_GRID=0 disables
 static bool grid_plan(const Model& m, int op, GridPlan* out) {
-  if (op != IRLMX_OP_SOFT_BACKWARD && op != IRLMX_OP_VALUE_ITERATION) return false;
-  if (m.dense || m.A > kGridMaxActions || !grid_kmax(m) || getenv_int("IRLMX_GRID", 1) == 0) return false;
+  if (m.dense || getenv_int("IRLMX_GRID", 1) == 0) return false;
   if (m.S <= fused_max_states()) return false;  // one workgroup holds it: the fused shape
-  const bool soft = op == IRLMX_OP_SOFT_BACKWARD;
+  if (op == IRLMX_OP_SOFT_BACKWARD || op == IRLMX_OP_VALUE_ITERATION) {
+    if (m.A > kGridMaxActions || !grid_kmax(m)) return false;
+  } else if (op == IRLMX_OP_FORWARD || op == IRLMX_OP_BACKWARD) {
+    // stencil grids run the cluster shape; ELL rows of at most 8 slots here
+    if (m.stencil || !(op == IRLMX_OP_FORWARD ? grid_kmax_fwd(m) : grid_kmax(m)) || m.A > kMaxActions) return false;
+  } else {
+    return false;
+  }
   for (int spt = 1; spt <= 4; spt *= 2) {
-    void* fn = soft ? bellman_grid_fn<true>(spt, grid_kmax(m)) : bellman_grid_fn<false>(spt, grid_kmax(m));
+    void* fn = grid_fn(m, op, spt);
     if (!fn) continue;
     const int bpi = (m.S + spt * kGridThreads - 1) / (spt * kGridThreads);
     if (bpi > kGridThreads) continue;  // the block maxima are gathered one per thread
@@ -1044,6 +1305,24 @@ static bool grid_plan(const Model& m, int op, GridPlan* out) {
 }
 
 static std::atomic<unsigned> g_grid_salt{1};
+
+// one persistent launch of the grid shape, then its exchange-timeout word
+// (synchronises the stream, like cluster_run)
+static int grid_launch(const Model& m, int op, const GridPlan& gp, void** args, const Ws& ws, hipStream_t st) {
+  const int grid = gp.xcd ? 8 * ((m.B + 7) / 8) * gp.bpi : gp.bpi * m.B;
+  hipError_t e = hipLaunchKernel(grid_fn(m, op, gp.spt), dim3(grid), dim3(kGridThreads), args, 0, st);
+  if (e != hipSuccess) return hip_fail(e, "grid launch");
+  int err = 0;
+  e = hipMemcpyAsync(&err, ws.err, sizeof(int), hipMemcpyDeviceToHost, st);
+  if (e == hipSuccess) e = hipStreamSynchronize(st);
+  if (e != hipSuccess) return hip_fail(e, "grid sync");
+  if (err) { set_error("grid shape: exchange timed out (workgroups not co-resident?)"); return IRLMX_EHIP; }
+  return 0;
+}
+
+static GridArgs grid_args(const Model& m, const GridPlan& gp, const Ws& ws) {
+  return GridArgs{ws.gran, ws.sgran, ws.err, gp.bpi, m.B, gp.xcd, g_grid_salt.fetch_add(1, std::memory_order_relaxed)};
+}
 
 __global__ void fill_kernel(double* p, size_t n, double v) {
   const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -1412,6 +1691,13 @@ extern "C" int irlmx_forward_svf(const irlmx_mdp* mdp, const double* p_initial, 
     if (e != hipSuccess) return hip_fail(e, "workspace memset");
     hipLaunchKernelGGL(fwd_weights_kernel, g, dim3(256), 0, st, m, p_action, terminal, ws.wgt, ws.bad);
   }
+  GridPlan gp;
+  if (grid_plan(m, IRLMX_OP_FORWARD, &gp)) {  // ELL models: one persistent launch
+    LinearGridArgs la{m, ws.wgt, p_initial, nullptr, ws.bad, eps, (long long)max_iter, 0, svf, iterations, status};
+    GridArgs ga = grid_args(m, gp, ws);
+    void* args[] = {&la, &ga};
+    return grid_launch(m, IRLMX_OP_FORWARD, gp, args, ws, st);
+  }
   const dim3 gs((m.S + kSweepThreads - 1) / kSweepThreads, m.B);
   int rc = run_until_done(ws, m.B, st, [&](long long it, int r3) {
     hipLaunchKernelGGL(fwd_sweep_kernel, gs, dim3(kSweepThreads), 0, st, a, ws, it, r3);
@@ -1458,6 +1744,13 @@ extern "C" int irlmx_backward_maxent(const irlmx_mdp* mdp, const double* reward,
                        p_action);
     e = hipGetLastError();
     return e == hipSuccess ? 0 : hip_fail(e, "backward nan fill");
+  }
+  GridPlan gp;
+  if (grid_plan(m, IRLMX_OP_BACKWARD, &gp)) {  // ELL models: one persistent launch
+    LinearGridArgs la{m, ws.wgt, reward, terminal, ws.bad, 0.0, 0, rescale, p_action, nullptr, status};
+    GridArgs ga = grid_args(m, gp, ws);
+    void* args[] = {&la, &ga};
+    return grid_launch(m, IRLMX_OP_BACKWARD, gp, args, ws, st);
   }
   const dim3 g((m.S + kSweepThreads - 1) / kSweepThreads, m.B);
   hipLaunchKernelGGL(bwd_init_kernel, g, dim3(kSweepThreads), 0, st, a, ws);
@@ -1515,18 +1808,9 @@ static int bellman_common(const irlmx_mdp* mdp, const double* reward, const doub
   }
   GridPlan gp;
   if (grid_plan(m, op, &gp)) {  // persistent grid shape: one launch for the whole loop
-    GridArgs ga{ws.gran, ws.sgran, ws.err, gp.bpi, m.B, gp.xcd, g_grid_salt.fetch_add(1, std::memory_order_relaxed)};
-    void* fn = soft ? bellman_grid_fn<true>(gp.spt, grid_kmax(m)) : bellman_grid_fn<false>(gp.spt, grid_kmax(m));
+    GridArgs ga = grid_args(m, gp, ws);
     void* args[] = {&a, &ga};
-    const int grid = gp.xcd ? 8 * ((m.B + 7) / 8) * gp.bpi : gp.bpi * m.B;
-    e = hipLaunchKernel(fn, dim3(grid), dim3(kGridThreads), args, 0, st);
-    if (e != hipSuccess) return hip_fail(e, "bellman grid launch");
-    int err = 0;
-    e = hipMemcpyAsync(&err, ws.err, sizeof(int), hipMemcpyDeviceToHost, st);
-    if (e == hipSuccess) e = hipStreamSynchronize(st);
-    if (e != hipSuccess) return hip_fail(e, "bellman grid sync");
-    if (err) { set_error("bellman grid: exchange timed out (workgroups not co-resident?)"); return IRLMX_EHIP; }
-    return 0;
+    return grid_launch(m, op, gp, args, ws, st);
   }
   int rc = run_until_done(ws, m.B, st, [&](long long it, int r3) {
     if (soft) hipLaunchKernelGGL(bellman_sweep_kernel<true>, gb, dim3(bt), 0, st, a, ws, it, r3);

@@ -175,3 +175,82 @@ def test_config2_stay_variant_vs_sparse_oracle(dev):
     assert int(ks[0]) == ref_ks
     assert np.max(np.abs(cpi[0].cpu().numpy() - ref_cpi)) <= 1e-9 * np.max(np.abs(ref_cpi))
     assert np.max(np.abs(cv[0].cpu().numpy() - ref_cv)) <= 1e-9 * np.max(np.abs(ref_cv))
+
+
+def ell_model(mats, dev):
+    """A DeviceMDP in the ELL layout built on the host from per-action CSR
+    matrices (the layout irlmx_dense_to_ell produces: targets / sources of each
+    state ascending, unused slots pointing at the state itself with value 0)."""
+    import scipy.sparse as sp
+    from irlmx import DeviceMDP, _lib
+    n, A = mats[0].shape[0], len(mats)
+    union = sum(abs(m) for m in mats).tocsr()
+    union.sort_indices()
+
+    def form(u, ms):
+        cnt = np.diff(u.indptr)
+        k = max(1, int(cnt.max()))
+        rows = np.repeat(np.arange(n), cnt)
+        slot = np.arange(u.indices.size) - np.repeat(u.indptr[:-1], cnt)
+        idx = np.tile(np.arange(n), (k, 1))
+        idx[slot, rows] = u.indices
+        val = np.zeros((A, k, n))
+        for a, m in enumerate(ms):
+            val[a, slot, rows] = np.asarray(m[rows, u.indices]).reshape(-1)
+        return k, idx, val
+
+    k_row, ri, rv = form(union, mats)
+    ut = union.T.tocsr()
+    ut.sort_indices()
+    k_col, ci, cv = form(ut, [m.T.tocsr() for m in mats])
+    t = lambda x, dt: torch.as_tensor(x[None], dtype=dt, device=dev).contiguous()
+    return DeviceMDP(_lib.LAYOUT_ELL, n, A, 1, True, t(rv, torch.float64), row_idx=t(ri, torch.int32),
+                     col_idx=t(ci, torch.int32), col_val=t(cv, torch.float64), k_row=k_row, k_col=k_col, device=dev)
+
+
+def test_ell_grid_shape_at_128(dev, monkeypatch):
+    """A 128x128 IcyGridWorld in the generic ELL layout (S = 16384 > one CU):
+    backward, forward, soft VI and VI run on the persistent grid shape, bit for
+    bit equal to the per-sweep shape (also the unscaled, overflowing backward),
+    and the backward and capped forward within 1e-9 of the CSR oracle."""
+    from irlmx import ops
+    from irlmx.batch import terminal_reward
+    size, n = 128, 128 * 128
+    mats = O.icy_gridworld_csr(size, 0.2)
+    mdp = ell_model(mats, dev).with_batch(2)
+    assert mdp.k_row <= 5 and mdp.k_col <= 5
+    for op in ("backward", "forward", "soft_backward", "value_iteration"):
+        assert ops.execution_plan(mdp, op)["shape"] == "grid", op
+    rng = np.random.default_rng(99)
+    r = rng.uniform(0.0, 1.0, (2, n))
+    tm = ops.terminal_mask([n - 1], n, batch=2, device=dev)
+    p0 = np.zeros((2, n))
+    p0[:, 0] = 1.0
+    phi = terminal_reward([n - 1], n, 2, dev)
+
+    def run():
+        pi = ops.backward_maxent(mdp, r, tm)
+        # (a converged forward on the unit-reward policy: random rewards mix over millions of sweeps)
+        pi1 = ops.backward_maxent(mdp, np.ones((2, n)), tm)
+        return (pi, ops.forward_svf(mdp, p0, tm, pi, max_iter=3000), ops.forward_svf(mdp, p0, tm, pi1, eps=1e-2),
+                ops.soft_backward(mdp, r, phi, 0.7), ops.value_iteration(mdp, r, 0.9),
+                ops.backward_maxent(mdp, r, tm, rescale=False))
+
+    got = run()
+    monkeypatch.setenv("IRLMX_GRID", "0")
+    assert ops.execution_plan(mdp, "forward")["shape"] == "sweep"
+    ref = run()
+
+    def bits(x):
+        return x.view(torch.int64) if x.dtype == torch.float64 else x
+
+    flat = lambda t: list(t) if isinstance(t, tuple) else [t]
+    for g_, r_ in zip(got, ref):
+        for x, y in zip(flat(g_), flat(r_)):
+            assert torch.equal(bits(x), bits(y))
+    assert bool(torch.isnan(got[5]).all())                  # the reference's overflow: NaN everywhere
+    pi = got[0][0].cpu().numpy()
+    pi_ref = O.backward_maxent_csr(mats, [n - 1], r[0])
+    assert rel_err(pi, pi_ref) <= RTOL
+    svf_ref, k_ref = O.forward_svf_csr(mats, p0[0], [n - 1], pi, max_iter=3000)
+    assert int(got[1][1][0]) == k_ref == 3000 and rel_err(got[1][0][0].cpu().numpy(), svf_ref) <= RTOL
