@@ -77,6 +77,7 @@ __device__ inline double wave_dot(const double* __restrict__ row, const double* 
     const double2* v2 = reinterpret_cast<const double2*>(v);
     const int n2 = S >> 1;
     int j = lane;
+#pragma unroll kDenseUnroll
     for (; j + 64 < n2; j += 128) {
       const double2 x = r2[j];
       const double2 y = r2[j + 64];
