@@ -51,16 +51,16 @@ constexpr int kDenseThreads = 256;
 //                         S=2048 bwd / fwd    S=4096 bwd / fwd
 //   LDS vector, unroll 1     8.97 / 9.86        29.3 / 30.3
 //   LDS vector, unroll 4     8.40 / 9.12        26.2 / 27.1
-//   global vector, unroll 4  8.18 / 9.31        24.8 / 26.5   (default)
+//   global vector, unroll 4  8.18 / 9.31        24.8 / 26.5
 //   one row per wave         10.9 / 12.0        31.3 / 32.7
 // Unrolling lets a wave issue the loads of four row chunks before their FMAs
-// (same FMA order, bit-identical); reading the swept vector through L1/L2
-// instead of staging it in LDS drops the per-block prologue and its barrier.
+// (same FMA order, bit-identical).  Reading the swept vector through L1/L2
+// instead of staging it in LDS drops the per-block prologue and its barrier at
+// one instance; with several instances the vector re-reads compete with the
+// row streams in L1/L2 (S = 2048, B = 16: backward 36 us with LDS, 47 without;
+// forward 108 vs 158), so there it is staged (dense_lds_vec).
 #ifndef IRLMX_DENSE_RPW
 #define IRLMX_DENSE_RPW 2
-#endif
-#ifndef IRLMX_DENSE_LDS_MAX
-#define IRLMX_DENSE_LDS_MAX 0
 #endif
 #ifndef IRLMX_DENSE_UNROLL
 #define IRLMX_DENSE_UNROLL 4
@@ -68,7 +68,10 @@ constexpr int kDenseThreads = 256;
 constexpr int kDenseRowsPerWave = IRLMX_DENSE_RPW;
 constexpr int kDenseUnroll = IRLMX_DENSE_UNROLL;  // wave_dot: loop iterations whose loads issue together
 constexpr int kDenseRowsPerBlock = (kDenseThreads / kWave) * kDenseRowsPerWave;
-constexpr int kDenseLdsMaxStates = IRLMX_DENSE_LDS_MAX;  // the swept vector is staged in LDS up to here
+constexpr int kDenseLdsMaxStates = 8192;  // the swept vector fits in LDS up to here (64 KiB)
+
+// Stage the swept vector in LDS?
+bool dense_lds_vec(const DenseView& d);
 
 void dense_rows_launch(const double* dense, int S, int A, double* P, double* M, hipStream_t st);
 void dense_fwd_weights_launch(const DenseView& d, const double* pi, const uint8_t* term, DenseBufs w,

@@ -50,7 +50,7 @@ __device__ inline bool dense_should_stop(int b, long long it, int r3, double eps
   return true;
 }
 
-// Copy the swept vector into LDS (S <= kDenseLdsMaxStates), else read it in place.
+// Copy the swept vector into LDS (dense_lds_vec), else read it in place.
 template <bool LDSV>
 __device__ inline const double* stage(const double* __restrict__ src, double* lds, int S) {
   if constexpr (!LDSV) {
@@ -421,20 +421,23 @@ dense_bellman_finish_kernel(DenseView d, DenseBellman a, DenseBufs w) {
 // One table shared by B instances (the backward sweep M . [zs_1 .. zs_B]).
 // v_mfma_f64_16x16x4_f64: lane l supplies A[l & 15][k = l >> 4] and
 // B[k = l >> 4][l & 15]; D[row (l >> 4) + 4 r][col l & 15] in register r
-// (cdna_hip_programming.md, f64 MFMA maps).  A workgroup owns 32 rows of M x 64
-// instances; its four waves split the sum over t (K) into quarters and meet in
-// LDS, summed in wave order (deterministic).  Per 16-wide K chunk a lane loads
+// (cdna_hip_programming.md, f64 MFMA maps).  A workgroup owns 16 ST rows of M x
+// 16 NBT instances; its kGemmWaves waves split the sum over t (K) into equal
+// parts and meet in LDS, summed in wave order (deterministic).  With one
+// workgroup per CU, eight waves (two per SIMD: one wave's loads in flight while
+// the other's MFMAs run) measured 1.1-1.7x faster than four, sixteen no better
+// (S = 4096: B = 4 48.9 -> 29.1 us, B = 16 47.4 -> 33.9, B = 64 85.0 -> 79.2);
+// with two or more workgroups per CU four waves stay faster (the stacked soft-VI
+// GEMM at S = 4096, B = 16: 210 vs 233 us).  Per 16-wide K chunk a lane loads
 // 32 contiguous bytes of each of its rows of M and Z (128 B per row across the
 // four lanes of a column), and MFMA x (x = 0..3) uses element x of them: the
 // k index of both operands maps to the same t = 16 c + 4 (l >> 4) + x.  M is
 // read from HBM once per sweep; Z (B x S) is re-read per 32 rows of M (L2).
-constexpr int kGemmWaves = 4;
-
 typedef double f64x4 __attribute__((ext_vector_type(4)));
 
 // ST 16-row tiles of M and NBT 16-instance column tiles per workgroup (sized to
 // S and B so that the grid fills the chip)
-template <int ST, int NBT>
+template <int ST, int NBT, int kGemmWaves>
 __global__ void __launch_bounds__(kGemmWaves * kWave)
 dense_gemm_kernel(const double* __restrict__ M, const double* __restrict__ Z, double* __restrict__ C, int R, int S,
                   int B) {  // M [R][S], Z [B][S] -> C [B][R]
@@ -529,8 +532,8 @@ dense_gemm_kernel(const double* __restrict__ M, const double* __restrict__ Z, do
 
 namespace {
 dim3 row_grid(const DenseView& d) { return dim3((d.S + kDenseRowsPerBlock - 1) / kDenseRowsPerBlock, d.B); }
-bool lds_vec(int S) { return S <= kDenseLdsMaxStates; }
-size_t lds_bytes(int S) { return lds_vec(S) ? (size_t)S * sizeof(double) : 0; }
+bool lds_vec(const DenseView& d) { return dense_lds_vec(d); }
+size_t lds_bytes(int S) { return (size_t)S * sizeof(double); }
 }  // namespace
 
 void dense_rows_launch(const double* dense, int S, int A, double* P, double* M, hipStream_t st) {
@@ -549,7 +552,7 @@ void dense_fwd_weights_launch(const DenseView& d, const double* pi, const uint8_
 
 void dense_fwd_sweep_launch(const DenseView& d, const double* p0, double eps, long long max_iter, int32_t* status,
                             DenseBufs w, long long it, int r3, hipStream_t st) {
-  if (lds_vec(d.S))
+  if (lds_vec(d))
     hipLaunchKernelGGL(dense_fwd_sweep_kernel<true>, row_grid(d), dim3(kDenseThreads), lds_bytes(d.S), st, d, p0, eps,
                        max_iter, status, w, it, r3);
   else
@@ -563,7 +566,7 @@ void dense_bwd_init_launch(const DenseView& d, const uint8_t* term, DenseBufs w,
 
 void dense_bwd_sweep_launch(const DenseView& d, const double* reward, int rescale, DenseBufs w, long long it, int r3,
                             hipStream_t st) {
-  if (lds_vec(d.S))
+  if (lds_vec(d))
     hipLaunchKernelGGL(dense_bwd_sweep_kernel<true>, row_grid(d), dim3(kDenseThreads), lds_bytes(d.S), st, d, reward,
                        rescale, w, it, r3);
   else
@@ -579,7 +582,7 @@ void dense_bwd_gemm_epilogue_launch(const DenseView& d, const double* reward, in
 
 void dense_bwd_final_launch(const DenseView& d, const double* reward, int rescale, double* pi, int32_t* status,
                             DenseBufs w, long long collapsed, int r3, hipStream_t st) {
-  if (lds_vec(d.S))
+  if (lds_vec(d))
     hipLaunchKernelGGL(dense_bwd_final_kernel<true>, row_grid(d), dim3(kDenseThreads), lds_bytes(d.S), st, d, reward,
                        rescale, pi, status, w, collapsed, r3);
   else
@@ -589,7 +592,7 @@ void dense_bwd_final_launch(const DenseView& d, const double* reward, int rescal
 
 void dense_bellman_sweep_launch(const DenseView& d, const DenseBellman& a, DenseBufs w, long long it, int r3,
                                 hipStream_t st) {
-  if (lds_vec(d.S))
+  if (lds_vec(d))
     hipLaunchKernelGGL(dense_bellman_sweep_kernel<true>, row_grid(d), dim3(kDenseThreads), lds_bytes(d.S), st, d, a,
                        w, it, r3);
   else
@@ -606,7 +609,7 @@ void dense_bellman_gemm_sweep_launch(const DenseView& d, const DenseBellman& a, 
 }
 
 void dense_bellman_finish_launch(const DenseView& d, const DenseBellman& a, DenseBufs w, hipStream_t st) {
-  if (lds_vec(d.S))
+  if (lds_vec(d))
     hipLaunchKernelGGL(dense_bellman_finish_kernel<true>, row_grid(d), dim3(kDenseThreads), lds_bytes(d.S), st, d, a,
                        w);
   else
@@ -619,13 +622,22 @@ namespace irlmx {
 
 bool dense_gemm_mfma_ok(int S) { return S % 4 == 0; }
 
-template <int ST, int NBT>
+bool dense_lds_vec(const DenseView& d) { return d.S <= kDenseLdsMaxStates && d.B > 1; }
+
+template <int ST, int NBT, int NW>
 static void gemm_go(const double* M, const double* Z, double* C, int R, int S, int B, hipStream_t st) {
-  const size_t lds = (size_t)kGemmWaves * ST * NBT * 4 * kWave * sizeof(double);
-  (void)hipFuncSetAttribute((const void*)&dense_gemm_kernel<ST, NBT>, hipFuncAttributeMaxDynamicSharedMemorySize,
+  const size_t lds = (size_t)NW * ST * NBT * 4 * kWave * sizeof(double);
+  (void)hipFuncSetAttribute((const void*)&dense_gemm_kernel<ST, NBT, NW>, hipFuncAttributeMaxDynamicSharedMemorySize,
                             (int)lds);
   const dim3 grid((R + 16 * ST - 1) / (16 * ST), (B + 16 * NBT - 1) / (16 * NBT));
-  hipLaunchKernelGGL((dense_gemm_kernel<ST, NBT>), grid, dim3(kGemmWaves * kWave), lds, st, M, Z, C, R, S, B);
+  hipLaunchKernelGGL((dense_gemm_kernel<ST, NBT, NW>), grid, dim3(NW * kWave), lds, st, M, Z, C, R, S, B);
+}
+
+template <int ST, int NBT>
+static void gemm_waves(const double* M, const double* Z, double* C, int R, int S, int B, hipStream_t st) {
+  const long long wgs = (long long)((R + 16 * ST - 1) / (16 * ST)) * ((B + 16 * NBT - 1) / (16 * NBT));
+  if (wgs >= 512) gemm_go<ST, NBT, 4>(M, Z, C, R, S, B, st);  // several workgroups per CU
+  else gemm_go<ST, NBT, 8>(M, Z, C, R, S, B, st);
 }
 
 void dense_gemm_launch(const double* M, const double* Z, double* C, int R, int S, int B, hipStream_t st) {
@@ -634,13 +646,13 @@ void dense_gemm_launch(const double* M, const double* Z, double* C, int R, int S
   // two row tiles per wave (half the Z re-reads) while that still gives >= 256 workgroups
   const bool st2 = (long long)((R + 31) / 32) * ny >= 256;
   if (st2) {
-    if (nbt == 1) gemm_go<2, 1>(M, Z, C, R, S, B, st);
-    else if (nbt == 2) gemm_go<2, 2>(M, Z, C, R, S, B, st);
-    else gemm_go<2, 4>(M, Z, C, R, S, B, st);
+    if (nbt == 1) gemm_waves<2, 1>(M, Z, C, R, S, B, st);
+    else if (nbt == 2) gemm_waves<2, 2>(M, Z, C, R, S, B, st);
+    else gemm_waves<2, 4>(M, Z, C, R, S, B, st);
   } else {
-    if (nbt == 1) gemm_go<1, 1>(M, Z, C, R, S, B, st);
-    else if (nbt == 2) gemm_go<1, 2>(M, Z, C, R, S, B, st);
-    else gemm_go<1, 4>(M, Z, C, R, S, B, st);
+    if (nbt == 1) gemm_waves<1, 1>(M, Z, C, R, S, B, st);
+    else if (nbt == 2) gemm_waves<1, 2>(M, Z, C, R, S, B, st);
+    else gemm_waves<1, 4>(M, Z, C, R, S, B, st);
   }
 }
 

@@ -1498,8 +1498,8 @@ static DenseBufs dense_bufs(const Ws& ws) {
 // profiles/r02_dense_gemm_bench.txt, microseconds per sweep):
 //
 //            streaming (VALU)      hand-written fp64 MFMA     rocBLAS dgemm
-//   S=2048   B=4 16  B=16 36  B=64 102   25 / 25 / 45           116 / 117 / 117
-//   S=4096   B=4 63  B=16 277 B=64 1173  48 / 47 / 85           448 / 447 / 451
+//   S=2048   B=4 16  B=16 40  B=64 112   16 / 19 / 43           117 / 117 / 117
+//   S=4096   B=4 81  B=16 303 B=64 1227  29 / 34 / 80           447 / 448 / 450
 //
 // Streaming re-reads M from the 256 MB last-level cache, so it wins for few
 // instances while M is small; the MFMA kernel (dense.hip dense_gemm_kernel) wins
@@ -1634,7 +1634,7 @@ extern "C" int irlmx_execution_plan(const irlmx_mdp* mdp, int32_t op, int64_t* p
                       : (op != IRLMX_OP_FORWARD && dense_gemm(m) && dense_gemm_mfma_ok(m.S));
     plan[0] = gemm ? IRLMX_SHAPE_DENSE_GEMM : IRLMX_SHAPE_DENSE;
     plan[7] = kDenseThreads;
-    plan[9] = m.S <= kDenseLdsMaxStates ? (int64_t)m.S * 8 : 0;
+    plan[9] = dense_lds_vec(dense_view(m)) ? (int64_t)m.S * 8 : 0;
     return 0;
   }
   plan[0] = IRLMX_SHAPE_SWEEP;

@@ -25,6 +25,8 @@ for S in sizes:
         for mode, env, eng in (("stream", "1000000", "mfma"), ("gemm-mfma", "1", "mfma"), ("gemm-rocblas", "1", "rocblas")):
             if B == 1 and mode != "stream":
                 continue
+            if os.environ.get("MODES") and mode not in os.environ["MODES"].split(","):
+                continue
             os.environ["IRLMX_DENSE_GEMM_MIN"] = env
             os.environ["IRLMX_DENSE_GEMM_ENGINE"] = eng
             ops.backward_maxent(mdp, r, tm); torch.cuda.synchronize()
