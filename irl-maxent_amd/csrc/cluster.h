@@ -45,7 +45,8 @@ struct ClusterArgs {
   unsigned long long* sgran;  // [B][3][H] x 16-byte tagged granule pairs (tile summaries, XCC ids)
   int xcd_group;           // number the tiles of an instance within one XCD group
   unsigned salt;           // per-launch granule tag salt
-  int* err;                // [1] exchange timeout
+  int* err;                // [0]: exchange timeout (1), non-finite (2), not co-resident (4); [1..2]: rendezvous
+  int n_resident;          // workgroups of this launch that must run at once (coresident())
   unsigned long long* stamps;  // optional [grid][8] phase cycle counters (IRLMX_STAMPS=1), else null
   double* out;             // forward: svf [B][S]; backward: pi [B][S][A]
   int64_t* iters;
@@ -110,6 +111,31 @@ __device__ inline bool gran_gather(__amdgpu_buffer_rsrc_t r, __amdgpu_buffer_rsr
   return true;
 }
 
+// Co-residency rendezvous of a persistent launch (cluster and grid shapes),
+// thread 0 of every participating workgroup: count in ctr[0] ("arrived") and
+// wait for all n, then count in ctr[1] ("committed") and wait for all n.  The
+// hand-offs assume that all workgroups run at once; when another kernel or
+// process holds CUs, some start only after others have left, and without this
+// check they would spin until the exchange timeout.  A workgroup that does not
+// see all arrivals within kArriveTicks leaves without committing, so nobody
+// passes the second phase and the host reruns the call on the per-sweep shape.
+// A workgroup that committed saw every arrival; the rest commit within a poll
+// of the last arrival, well inside the second phase's longer limit, so either
+// all workgroups pass or none does.  ctr is zeroed before every launch.
+constexpr unsigned long long kArriveTicks = 10000000ull;  // 100 ms of s_memrealtime (100 MHz)
+constexpr int kErrNotResident = 4;                        // err bit: the rendezvous failed
+__device__ inline bool coresident(int* ctr, int n) {
+  const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+  for (int ph = 0; ph < 2; ++ph) {
+    atomicAdd(&ctr[ph], 1);
+    while (__hip_atomic_load(&ctr[ph], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < n) {
+      if (__builtin_amdgcn_s_memrealtime() - t0 > (ph + 1) * kArriveTicks) return false;
+      __builtin_amdgcn_s_sleep(2);
+    }
+  }
+  return true;
+}
+
 __device__ inline unsigned long long stamp_now() { return __builtin_amdgcn_s_memtime(); }
 
 // Wave-wide reduction of a 32-bit value with DPP (no LDS): butterflies inside
@@ -153,6 +179,9 @@ __device__ inline unsigned long long wave_or_u64(unsigned long long v) {
 // cluster_run's result when a forward instance turned non-finite: the call must
 // be rerun on the per-sweep shape (exact NaN bookkeeping; cluster.hip)
 constexpr int kClusterNonFinite = 1;
+// cluster_run's result when the launch's workgroups could not all run at once
+// (coresident()): the call must be rerun on a shape without hand-offs
+constexpr int kClusterNotResident = 2;
 
 bool cluster_plan(int W, int H, int B, int mode, ClusterPlan* out);
 int cluster_run(int mode, const ClusterPlan& p, ClusterArgs a, int B, hipStream_t st);

@@ -129,6 +129,15 @@ __global__ void __launch_bounds__(NT) cluster_kernel(ClusterArgs a) {
   const int tile = lin % a.C;
   const int inst = a.b0 + lin / a.C;
   const int tid = threadIdx.x;
+  {  // every workgroup of the launch running at once, or none goes on (coresident())
+    __shared__ int resident;
+    if (tid == 0) resident = coresident(a.err + 1, a.n_resident) ? 1 : 0;
+    __syncthreads();
+    if (!resident) {
+      if (tid == 0) atomicOr(a.err, kErrNotResident);
+      return;
+    }
+  }
   const int r0 = tile * a.R, r1 = min(H, r0 + a.R);
   const int e0 = max(0, r0 - a.G), e1 = min(H, r1 + a.G);
   const int E = (e1 - e0) * W;
@@ -983,10 +992,18 @@ int cluster_run(int mode, const ClusterPlan& plan, ClusterArgs a, int B, hipStre
     (void)hipMemsetAsync(stamps, 0, sizeof(unsigned long long) * 8 * nwg, st);
   }
   a.stamps = stamps;
+  // IRLMX_TEST_NOT_RESIDENT=1 (tests only): wait for one workgroup more than
+  // the launch has, i.e. take the not-co-resident path deterministically
+  const int extra = env_int("IRLMX_TEST_NOT_RESIDENT", 0) ? 1 : 0;
   for (int b0 = 0; b0 < B; b0 += p.per_launch) {
     const int nb = std::min(p.per_launch, B - b0);
     a.b0 = b0;
     a.nb = nb;
+    a.n_resident = nb * p.C + extra;
+    if (b0 > 0) {  // fresh rendezvous counters for this launch (err[1..2])
+      e = hipMemsetAsync(a.err + 1, 0, 2 * sizeof(int), st);
+      if (e != hipSuccess) return hip_fail(e, "cluster rendezvous reset");
+    }
     a.xcd_group = xcd_groupable(nb, p.C) && env_int("IRLMX_XCD_GROUP", 1) != 0;
     a.salt = g_salt.fetch_add(1, std::memory_order_relaxed);
     void* args[] = {&a};
@@ -1022,6 +1039,7 @@ int cluster_run(int mode, const ClusterPlan& plan, ClusterArgs a, int B, hipStre
     free(h);
     (void)hipFree(stamps);
   }
+  if (err & kErrNotResident) return kClusterNotResident;
   if (err & 1) { set_error("cluster: halo exchange timed out (workgroups not co-resident?)"); return IRLMX_EHIP; }
   return (err & 2) ? kClusterNonFinite : 0;
 }

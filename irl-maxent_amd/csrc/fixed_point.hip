@@ -817,7 +817,18 @@ struct GridArgs {
   int nb;                     // instances
   int xcd_group;              // workgroups dealt to XCD groups (see the kernel)
   unsigned salt;
+  int n_resident;             // workgroups that must run at once (coresident(), cluster.h)
 };
+
+// every workgroup of the launch running at once, or none goes on (the err[1..2]
+// counters; err bit kErrNotResident tells the host to rerun per sweep)
+__device__ inline bool grid_coresident(const GridArgs& g) {
+  __shared__ int resident;
+  if (threadIdx.x == 0) resident = coresident(g.err + 1, g.n_resident) ? 1 : 0;
+  __syncthreads();
+  if (!resident && threadIdx.x == 0) atomicOr(g.err, kErrNotResident);
+  return resident != 0;
+}
 
 template <bool SOFT, int SPT, int KMAX>
 __global__ void __launch_bounds__(kGridThreads) bellman_grid_kernel(SoftArgs a, GridArgs g) {
@@ -835,6 +846,7 @@ __global__ void __launch_bounds__(kGridThreads) bellman_grid_kernel(SoftArgs a, 
     lin = il * g.bpi + kk % g.bpi;
   }
   const int b = lin / g.bpi, blk = lin % g.bpi, tid = threadIdx.x;
+  if (!grid_coresident(g)) return;
   constexpr int K = KMAX;
   __shared__ unsigned long long red_in[kGridThreads / kWave], red_out[kGridThreads / kWave];
   __shared__ int lflag;
@@ -1027,6 +1039,7 @@ __global__ void __launch_bounds__(kGridThreads) linear_grid_kernel(LinearGridArg
     lin = il * g.bpi + kk % g.bpi;
   }
   const int b = lin / g.bpi, blk = lin % g.bpi, tid = threadIdx.x;
+  if (!grid_coresident(g)) return;
   constexpr int K = KMAX;
   __shared__ unsigned long long red_in[kGridThreads / kWave], red_out[kGridThreads / kWave];
   __shared__ int lflag;
@@ -1316,12 +1329,19 @@ static int grid_launch(const Model& m, int op, const GridPlan& gp, void** args, 
   e = hipMemcpyAsync(&err, ws.err, sizeof(int), hipMemcpyDeviceToHost, st);
   if (e == hipSuccess) e = hipStreamSynchronize(st);
   if (e != hipSuccess) return hip_fail(e, "grid sync");
+  if (err & kErrNotResident) {
+    // not all workgroups could run at once: clear the words for the per-sweep rerun
+    e = hipMemsetAsync(ws.err, 0, 4 * sizeof(int), st);
+    return e == hipSuccess ? kClusterNotResident : hip_fail(e, "grid err reset");
+  }
   if (err) { set_error("grid shape: exchange timed out (workgroups not co-resident?)"); return IRLMX_EHIP; }
   return 0;
 }
 
 static GridArgs grid_args(const Model& m, const GridPlan& gp, const Ws& ws) {
-  return GridArgs{ws.gran, ws.sgran, ws.err, gp.bpi, m.B, gp.xcd, g_grid_salt.fetch_add(1, std::memory_order_relaxed)};
+  // (IRLMX_TEST_NOT_RESIDENT=1, tests only: one workgroup more than launched -> the per-sweep rerun)
+  return GridArgs{ws.gran, ws.sgran, ws.err, gp.bpi, m.B, gp.xcd, g_grid_salt.fetch_add(1, std::memory_order_relaxed),
+                  gp.bpi * m.B + (getenv_int("IRLMX_TEST_NOT_RESIDENT", 0) ? 1 : 0)};
 }
 
 __global__ void fill_kernel(double* p, size_t n, double v) {
@@ -1675,6 +1695,7 @@ extern "C" int irlmx_forward_svf(const irlmx_mdp* mdp, const double* p_initial, 
     return e == hipSuccess ? 0 : hip_fail(e, "dense forward");
   }
   ClusterPlan cp;
+  bool persistent = true;  // false once a persistent launch found its workgroups not co-resident
   if (m.stencil && cluster_plan(m.W, m.H, m.B, kModeFwd, &cp)) {
     ClusterArgs ca{};
     ca.W = m.W; ca.H = m.H; ca.S = m.S; ca.A = m.A;
@@ -1683,20 +1704,23 @@ extern "C" int irlmx_forward_svf(const irlmx_mdp* mdp, const double* p_initial, 
     ca.gran = ws.gran; ca.sgran = ws.sgran; ca.err = ws.err;
     ca.out = svf; ca.iters = iterations; ca.status = status;
     const int rc = cluster_run(kModeFwd, cp, ca, m.B, st);
-    if (rc != kClusterNonFinite) return rc;
+    if (rc != kClusterNonFinite && rc != kClusterNotResident) return rc;
     // an instance turned non-finite (rare): the cluster shape's convergence bits
     // drop NaN deltas, so rerun the call on the per-sweep shape, whose
-    // bookkeeping is exact (same arithmetic, bit-identical results)
+    // bookkeeping is exact (same arithmetic, bit-identical results); likewise
+    // when the tiles could not all run at once (another kernel holds CUs)
+    persistent = rc != kClusterNotResident;
     e = hipMemsetAsync(workspace, 0, ws.total, st);
     if (e != hipSuccess) return hip_fail(e, "workspace memset");
     hipLaunchKernelGGL(fwd_weights_kernel, g, dim3(256), 0, st, m, p_action, terminal, ws.wgt, ws.bad);
   }
   GridPlan gp;
-  if (grid_plan(m, IRLMX_OP_FORWARD, &gp)) {  // ELL models: one persistent launch
+  if (persistent && grid_plan(m, IRLMX_OP_FORWARD, &gp)) {  // ELL models: one persistent launch
     LinearGridArgs la{m, ws.wgt, p_initial, nullptr, ws.bad, eps, (long long)max_iter, 0, svf, iterations, status};
     GridArgs ga = grid_args(m, gp, ws);
     void* args[] = {&la, &ga};
-    return grid_launch(m, IRLMX_OP_FORWARD, gp, args, ws, st);
+    const int rc = grid_launch(m, IRLMX_OP_FORWARD, gp, args, ws, st);
+    if (rc != kClusterNotResident) return rc;  // else: the per-sweep shape below
   }
   const dim3 gs((m.S + kSweepThreads - 1) / kSweepThreads, m.B);
   int rc = run_until_done(ws, m.B, st, [&](long long it, int r3) {
@@ -1727,6 +1751,7 @@ extern "C" int irlmx_backward_maxent(const irlmx_mdp* mdp, const double* reward,
     return 0;
   }
   ClusterPlan cp;
+  bool persistent = true;  // false once a persistent launch found its workgroups not co-resident
   // (without rescaling the partition vector overflows like the reference's: such
   // calls take the per-sweep shape, whose non-finite bookkeeping is per sweep)
   if (m.stencil && m.A <= kMaxActions && rescale && cluster_plan(m.W, m.H, m.B, kModeBwd, &cp)) {
@@ -1738,19 +1763,29 @@ extern "C" int irlmx_backward_maxent(const irlmx_mdp* mdp, const double* reward,
     ca.n_sweeps = 2LL * m.S - 1; ca.rescale = rescale;
     ca.gran = ws.gran; ca.sgran = ws.sgran; ca.err = ws.err;
     ca.out = p_action; ca.status = status;
-    if (int rc = cluster_run(kModeBwd, cp, ca, m.B, st)) return rc;
-    // instances with non-finite weights: all NaN (bwd_nonfinite_rule), outside the sweep kernel
-    hipLaunchKernelGGL(bwd_nan_fill_kernel, dim3((m.S * m.A + 255) / 256, m.B), dim3(256), 0, st, m, ws.bad,
-                       p_action);
-    e = hipGetLastError();
-    return e == hipSuccess ? 0 : hip_fail(e, "backward nan fill");
+    const int rc = cluster_run(kModeBwd, cp, ca, m.B, st);
+    if (rc != kClusterNotResident) {
+      if (rc) return rc;
+      // instances with non-finite weights: all NaN (bwd_nonfinite_rule), outside the sweep kernel
+      hipLaunchKernelGGL(bwd_nan_fill_kernel, dim3((m.S * m.A + 255) / 256, m.B), dim3(256), 0, st, m, ws.bad,
+                         p_action);
+      e = hipGetLastError();
+      return e == hipSuccess ? 0 : hip_fail(e, "backward nan fill");
+    }
+    // the tiles could not all run at once (another kernel holds CUs): rerun on
+    // the per-sweep shape (same arithmetic, bit-identical results)
+    persistent = false;
+    e = hipMemsetAsync(workspace, 0, ws.total, st);
+    if (e != hipSuccess) return hip_fail(e, "workspace memset");
+    hipLaunchKernelGGL(bwd_weights_kernel, dim3((m.S + 255) / 256, m.B), dim3(256), 0, st, m, reward, ws.wgt, ws.bad);
   }
   GridPlan gp;
-  if (grid_plan(m, IRLMX_OP_BACKWARD, &gp)) {  // ELL models: one persistent launch
+  if (persistent && grid_plan(m, IRLMX_OP_BACKWARD, &gp)) {  // ELL models: one persistent launch
     LinearGridArgs la{m, ws.wgt, reward, terminal, ws.bad, 0.0, 0, rescale, p_action, nullptr, status};
     GridArgs ga = grid_args(m, gp, ws);
     void* args[] = {&la, &ga};
-    return grid_launch(m, IRLMX_OP_BACKWARD, gp, args, ws, st);
+    const int rc = grid_launch(m, IRLMX_OP_BACKWARD, gp, args, ws, st);
+    if (rc != kClusterNotResident) return rc;  // else: the per-sweep shape below
   }
   const dim3 g((m.S + kSweepThreads - 1) / kSweepThreads, m.B);
   hipLaunchKernelGGL(bwd_init_kernel, g, dim3(kSweepThreads), 0, st, a, ws);
@@ -1810,7 +1845,8 @@ static int bellman_common(const irlmx_mdp* mdp, const double* reward, const doub
   if (grid_plan(m, op, &gp)) {  // persistent grid shape: one launch for the whole loop
     GridArgs ga = grid_args(m, gp, ws);
     void* args[] = {&a, &ga};
-    return grid_launch(m, op, gp, args, ws, st);
+    const int rc = grid_launch(m, op, gp, args, ws, st);
+    if (rc != kClusterNotResident) return rc;  // else: the per-sweep shape below
   }
   int rc = run_until_done(ws, m.B, st, [&](long long it, int r3) {
     if (soft) hipLaunchKernelGGL(bellman_sweep_kernel<true>, gb, dim3(bt), 0, st, a, ws, it, r3);
