@@ -306,6 +306,11 @@ def kernel_name(mode, plan, width):
 
 def main(argv=None):
     args = parse(argv)
+    # stdout carries exactly one JSON line: whatever libraries print there (gloo's
+    # rendezvous messages under torch.distributed.run) goes to stderr instead
+    sys.stdout.flush()
+    json_out = os.fdopen(os.dup(1), "w")
+    os.dup2(2, 1)
     import torch
     import torch.distributed as dist
 
@@ -318,6 +323,9 @@ def main(argv=None):
         # host-side group: only the timing barrier and the max-over-ranks travel
         # (no data-path collective) -- RCCL is not needed
         dist.init_process_group(backend="gloo")
+    # one GPU per rank; more ranks than GPUs (a rehearsal of the multi-rank path
+    # on a 1-GPU box) share them round-robin
+    local = local % max(1, torch.cuda.device_count())
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
 
@@ -484,7 +492,7 @@ def main(argv=None):
                 out["first_steps"]["speedup_vs_cpu"] = out["first_steps"]["instance_steps_per_s"] * t_cpu / n_first
             if not args.no_config1:
                 out["config1"] = config1_timings()
-        print(json.dumps(out), flush=True)
+        print(json.dumps(out), file=json_out, flush=True)
     if world > 1:
         dist.destroy_process_group()
 
