@@ -628,7 +628,29 @@ __global__ void __launch_bounds__(NT) cluster_kernel(ClusterArgs a) {
     __syncthreads();  // the tile summary in red32[m & 1] (and COLS: the staged rows) complete
     if (!solo) {
       if (tid == 0) gran_store(rs, ((unsigned)(m & 1) * (unsigned)a.H + (unsigned)tile) * 16u, red32[m & 1], tag, plain);
-      if constexpr (COLS) store_rows();
+      if constexpr (COLS && CPL == 2) {
+        store_rows();
+      } else if constexpr (COLS) {
+        // column quads (width 256: 8 rows per thread): the staged rows, kPub per
+        // thread at a time, all LDS reads in flight before the stores (the plain
+        // loop waits out one LDS round trip per row): config 4 backward 302.6 ->
+        // 293.6 ms; no gain for column pairs at width 128 (23.5 vs 23.7 ms)
+        constexpr int kPub = 4;
+        const int nA = pubA1 - own0, ntot = nA + (own1 - pubB0);
+        for (int k0 = 0; k0 < ntot; k0 += kPub * NT) {
+          int ls[kPub];
+          double vv[kPub];
+#pragma unroll
+          for (int i = 0; i < kPub; ++i) {
+            const int k = k0 + tid + i * NT;
+            ls[i] = k < nA ? own0 + k : (k < ntot ? pubB0 + (k - nA) : -1);
+            vv[i] = cur[pad + (ls[i] >= 0 ? ls[i] : 0)];
+          }
+#pragma unroll
+          for (int i = 0; i < kPub; ++i)
+            if (ls[i] >= 0) gran_store(rg, (gpar + (unsigned)(base + ls[i])) * 16u, dbits(vv[i]), tag, plain);
+        }
+      }
     }
     stamp(1);
     // ---- gather this tile's ghost rows and (threads < C) every tile's summary,
