@@ -47,6 +47,7 @@ CONFIGS = {
     # name: (grid size, instances per GPU, description, causal)
     "c3": (128, 64, "BASELINE config 3: 128x128 IcyGridWorld, batch 64 per GPU, fp64", False),
     "c2": (64, 1, "BASELINE config 2 (A=4 pinned variant): 64x64 IcyGridWorld, 1 instance", False),
+    "c2s": (64, 1, "BASELINE config 2 (|A|=5): 64x64 IcyGridWorld's four moves + stay, 1 instance, fp64", False),
     "c4": (256, 32, "BASELINE config 4: 256x256 IcyGridWorld, 32 instances per GPU", False),
     "c5": (128, 1, "BASELINE config 5: MaxCausalEnt (soft VI, discount 0.7) on 128x128 IcyGridWorld, "
                    "1 instance per GPU, fp64", True),
@@ -104,15 +105,16 @@ def blas_threads():
         return int(os.environ.get("OMP_NUM_THREADS", "1"))
 
 
-def cpu_sweep_times(size, p_slip, n_sweeps, causal=False):
+def cpu_sweep_times(size, p_slip, n_sweeps, causal=False, stay=False):
     """Seconds per sweep of the reference's dense statements on one instance
     (oracle restatement): forward maxent.py:109-112, backward :155-156 (or soft
     VI :329-338), and one call's table copies maxent.py:98-102, 143 (320).
 
     Above 128x128 the dense table does not fit in host memory: the statements
-    are timed at 128x128 and scaled by the dense work ratio (S / 16384)^2."""
+    are timed at 128x128 and scaled by the dense work ratio (S / 16384)^2.
+    ``stay``: config 2's fifth action (P[s, s, 4] = 1) appended to the table."""
     if size > CPU_DENSE_MAX:
-        t = cpu_sweep_times(CPU_DENSE_MAX, p_slip, n_sweeps, causal)
+        t = cpu_sweep_times(CPU_DENSE_MAX, p_slip, n_sweeps, causal, stay)
         ratio = (size * size / float(CPU_DENSE_MAX * CPU_DENSE_MAX)) ** 2
         t.update(t_f=t["t_f"] * ratio, t_b=t["t_b"] * ratio, t_copy=t["t_copy"] * ratio, ratio=ratio,
                  extrapolated_from=CPU_DENSE_MAX)
@@ -122,18 +124,21 @@ def cpu_sweep_times(size, p_slip, n_sweeps, causal=False):
     S = size * size
     t0 = time.perf_counter()
     P = O.icy_gridworld_table(size, p_slip)
+    if stay:
+        P = np.concatenate([P, np.identity(S)[:, :, None]], axis=2)
+    A = P.shape[2]
     t_build = time.perf_counter() - t0
     terminal = [S - 1]
     t0 = time.perf_counter()
     p = np.copy(P)
     p[terminal, :, :] = 0.0
-    fw = [np.array(p[:, :, a]) for a in range(4)]
+    fw = [np.array(p[:, :, a]) for a in range(A)]
     del p
-    bw = [np.array(P[:, :, a]) for a in range(4)]
+    bw = [np.array(P[:, :, a]) for a in range(A)]
     t_copy = time.perf_counter() - t0
     del P
     rng = np.random.default_rng(0)
-    pi = rng.uniform(0.0, 0.5, (S, 4))
+    pi = rng.uniform(0.0, 0.5, (S, A))
     p0 = np.zeros(S)
     p0[0] = 1.0
     d = rng.uniform(0.0, 1.0, S)
@@ -143,18 +148,18 @@ def cpu_sweep_times(size, p_slip, n_sweeps, causal=False):
     r = np.ones(S)
 
     def fwd_sweep(d):   # maxent.py:109-112
-        parts = [fw[a].T.dot(pi[:, a] * d) for a in range(4)]
+        parts = [fw[a].T.dot(pi[:, a] * d) for a in range(A)]
         nxt = p0 + np.array(parts).sum(axis=0)
         return np.max(np.abs(nxt - d)), nxt
 
     def bwd_sweep(zs):  # maxent.py:155-156
-        za = np.array([er * bw[a].dot(zs) for a in range(4)]).T
+        za = np.array([er * bw[a].dot(zs) for a in range(A)]).T
         return za.sum(axis=1) * 1e-3
 
     def soft_sweep(v):  # maxent.py:329-338
-        q = np.array([r + DISCOUNT * bw[a].dot(v) for a in range(4)]).T
+        q = np.array([r + DISCOUNT * bw[a].dot(v) for a in range(A)]).T
         nv = phi
-        for a in range(4):
+        for a in range(A):
             nv = O.softmax2(nv, q[:, a])
         nv = np.array(nv, dtype=float)
         np.max(np.abs(nv - v))
@@ -175,7 +180,7 @@ def cpu_sweep_times(size, p_slip, n_sweeps, causal=False):
         zs = back(zs)
     t_b = (time.perf_counter() - t0) / n_sweeps
     return {"t_f": t_f, "t_b": t_b, "t_copy": t_copy, "t_build": t_build, "n_sweeps": n_sweeps, "size": size,
-            "causal": causal, "ratio": 1.0, "extrapolated_from": None}
+            "causal": causal, "ratio": 1.0, "extrapolated_from": None, "n_actions": A}
 
 
 def cpu_baseline_from(t, k_b, k_f):
@@ -183,7 +188,7 @@ def cpu_baseline_from(t, k_b, k_f):
     one step = K_b * t_b + K_f * t_f + t_copy."""
     t_step = k_b * t["t_b"] + k_f * t["t_f"] + t["t_copy"]
     S = t["size"] * t["size"]
-    sample = (f"dense fp64 {t['size']}x{t['size']} (S={S}, A=4), one instance: {t['n_sweeps']} timed sweeps "
+    sample = (f"dense fp64 {t['size']}x{t['size']} (S={S}, A={t.get('n_actions', 4)}), one instance: {t['n_sweeps']} timed sweeps "
               f"each of maxent.py:109-112 (forward, {t['t_f'] / t['ratio'] * 1e3:.1f} ms) and "
               f"{':329-338 (soft VI' if t['causal'] else ':155-156 (backward'}, "
               f"{t['t_b'] / t['ratio'] * 1e3:.1f} ms) + one call's copies maxent.py:98-102,"
@@ -198,8 +203,8 @@ def cpu_baseline_from(t, k_b, k_f):
             "host_cpu_count": os.cpu_count(), "kind": "port", "sample": sample}
 
 
-def cpu_baseline(size, p_slip, k_b, k_f, n_sweeps, causal=False):
-    return cpu_baseline_from(cpu_sweep_times(size, p_slip, n_sweeps, causal), k_b, k_f)
+def cpu_baseline(size, p_slip, k_b, k_f, n_sweeps, causal=False, stay=False):
+    return cpu_baseline_from(cpu_sweep_times(size, p_slip, n_sweeps, causal, stay), k_b, k_f)
 
 
 def config1_timings(device_runs=True):
@@ -345,8 +350,11 @@ def main(argv=None):
     slips = instance_slips(ids, B_total)
     terminal = [S - 1]
 
+    stay = args.config == "c2s"
     mdp = DeviceMDP.icy_gridworld(size, slips, device=dev)
-    rv = mdp.row_val.cpu().numpy()
+    rv = mdp.row_val.cpu().numpy()       # the four moves: the synthetic expert never stays
+    if stay:
+        mdp = mdp.with_stay()
     e_f = np.empty((per_gpu, S))
     p_0 = np.empty((per_gpu, S))
     for i, b in enumerate(ids):
@@ -457,7 +465,7 @@ def main(argv=None):
             "vs_baseline": None,
             "dtype": "f64",
             "data": "synthetic (device-built IcyGridWorld tables, seeded synthetic expert demos)",
-            "config": {"workload": desc, "grid": f"{size}x{size}", "n_states": S, "n_actions": 4,
+            "config": {"workload": desc, "grid": f"{size}x{size}", "n_states": S, "n_actions": mdp.n_actions,
                        "batch_per_gpu": per_gpu, "global_batch": B_total, "eps_svf": 1e-5,
                        "parallelism": f"instances sharded over {world} GPU(s), no collective"},
             "plans": plans,
@@ -481,7 +489,7 @@ def main(argv=None):
                          "from the unit reward (~360k sweeps at 128x128)")}
         out["roofline"]["stream_copy_GBs"] = stream_copy_gbs(dev)
         if world == 1 and not args.no_cpu_baseline:
-            t = cpu_sweep_times(size, float(slips[0]), args.cpu_sweeps, causal)
+            t = cpu_sweep_times(size, float(slips[0]), args.cpu_sweeps, causal, stay)
             out["cpu_baseline"] = cpu_baseline_from(t, float(k_b.mean()), float(k_f.mean()))
             out["speedup_vs_cpu"] = out["value"] / out["cpu_baseline"]["value"]
             if n_first:

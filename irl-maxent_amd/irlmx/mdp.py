@@ -83,6 +83,19 @@ class DeviceMDP:
                    "build_gridworld")
         return cls(_lib.LAYOUT_STENCIL5, S, 4, batch, False, row_val, width=size, height=size, device=device)
 
+    def with_stay(self):
+        """The same STENCIL5 tables with a fifth action "stay" (P[s, s, 4] = 1):
+        BASELINE config 2's |A| = 5 variant of the gridworlds (SURVEY.md 8(d)2;
+        equal bit for bit to uploading the dense [S, S, 5] table, tested)."""
+        if self.layout != _lib.LAYOUT_STENCIL5:
+            raise ValueError("with_stay: STENCIL5 tables only")
+        B, A, K, S = self.row_val.shape
+        stay = torch.zeros((B, 1, K, S), dtype=self.row_val.dtype, device=self.row_val.device)
+        stay[:, 0, 0, :] = 1.0                                     # slot 0 = the state itself
+        row_val = torch.cat([self.row_val, stay], dim=1).contiguous()
+        return DeviceMDP(self.layout, S, A + 1, B, self.shared, row_val, width=self.width, height=self.height,
+                         device=self.device)
+
     #: ELL slots per state above which (and above S / 8) a table is kept DENSE
     DENSE_MIN_SLOTS = 32
 

@@ -13,7 +13,8 @@ import bench  # noqa: E402
 
 def test_configs_cover_baseline_rows():
     # BASELINE.json configs 2-5 (config 1, the 5x5 main.py run, is timed by bench.config1_timings)
-    assert set(bench.CONFIGS) == {"c2", "c3", "c4", "c5"}
+    # (c2s: config 2's |A| = 5 variant, the four moves + stay)
+    assert set(bench.CONFIGS) == {"c2", "c2s", "c3", "c4", "c5"}
     size, per_gpu, _, causal = bench.CONFIGS["c3"]
     assert (size, per_gpu, causal) == (128, 64, False)
     assert bench.CONFIGS["c5"][3] is True and bench.CONFIGS["c5"][0] == 128
@@ -26,6 +27,12 @@ def test_cpu_baseline_small(causal):
     assert out["cores"] >= 1 and out["host_cpu_count"] == os.cpu_count()
     assert (":329-338 (soft VI" in out["sample"]) == causal
     assert "K_b=288, K_f=500" in out["sample"]
+
+
+def test_cpu_baseline_stay_variant():
+    t = bench.cpu_sweep_times(8, 0.2, 1, stay=True)
+    assert t["n_actions"] == 5
+    assert "A=5" in bench.cpu_baseline_from(t, 128, 100.0)["sample"]
 
 
 def test_cpu_baseline_extrapolates_above_dense_limit(monkeypatch):

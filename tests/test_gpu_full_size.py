@@ -150,6 +150,9 @@ def test_config2_stay_variant_vs_sparse_oracle(dev):
     mdp = DeviceMDP.from_dense(dense, device=dev)
     del dense
     assert mdp.layout == _lib.LAYOUT_STENCIL5 and mdp.n_actions == 5
+    # the bench's construction (bench.py --config c2s): device-built four moves + stay, bit for bit
+    built = DeviceMDP.icy_gridworld(size, 0.2, device=dev).with_stay()
+    assert built.n_actions == 5 and torch.equal(built.row_val.view(torch.int64), mdp.row_val.view(torch.int64))
     rng = np.random.default_rng(12)
     r = rng.uniform(0.0, 1.0, n)
     term = [n - 1]
