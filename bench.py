@@ -82,6 +82,12 @@ def parse(argv=None):
     ap.add_argument("--first-steps", type=int, default=FIRST_STEPS,
                     help="steps from theta0 reported in first_steps (0: off)")
     ap.add_argument("--cpu-sweeps", type=int, default=60, help="timed CPU sweeps per statement")
+    ap.add_argument("--full-run", action="store_true",
+                    help="also run irl to convergence (maxent.py:240-252, eps 1e-4) on a fresh copy of the workload and "
+                         "report it under full_run (not part of the headline)")
+    ap.add_argument("--full-run-eps", type=float, default=1e-4)
+    ap.add_argument("--full-run-max-steps", type=int, default=20000, help="cap on gradient steps of the full run")
+    ap.add_argument("--no-compact", action="store_true", help="full run without compacting converged instances")
     ap.add_argument("--profile", default=None,
                     help="profiles/<tag>_summary.json of a rocprofv3 run of this workload (default: newest); its "
                          "kernel average and PMC HBM bytes are reported beside the live figures")
@@ -95,6 +101,34 @@ def _latest(pattern):
 
 
 CPU_DENSE_MAX = 128   # larger dense fp64 tables do not fit host RAM (256x256: 137 GB); extrapolate
+
+
+def cgroup_cpu_quota():
+    """CPUs the cgroup CPU controller grants this process (cpu.max quota / period),
+    or None when unlimited or unknown (cgroup v2, then v1)."""
+    try:
+        q, per = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        return None if q == "max" else float(q) / float(per)
+    except (OSError, ValueError):
+        pass
+    try:
+        q = int(open("/sys/fs/cgroup/cpu/cpu.cfs_quota_us").read())
+        per = int(open("/sys/fs/cgroup/cpu/cpu.cfs_period_us").read())
+        return None if q <= 0 else q / per
+    except (OSError, ValueError):
+        return None
+
+
+def usable_cpus():
+    """(usable CPUs, affinity CPUs, cgroup quota CPUs or None): the CPUs this
+    process may run on (sched_getaffinity) capped by its cgroup CPU quota -- the
+    "host cores" BASELINE.md asks the CPU baseline to use, which on a shared GPU
+    box is far below os.cpu_count()."""
+    import math
+    aff = len(os.sched_getaffinity(0))
+    quota = cgroup_cpu_quota()
+    usable = aff if quota is None else max(1, min(aff, int(math.floor(quota + 1e-9))))
+    return usable, aff, quota
 
 
 def blas_threads():
@@ -183,6 +217,25 @@ def cpu_sweep_times(size, p_slip, n_sweeps, causal=False, stay=False):
             "causal": causal, "ratio": 1.0, "extrapolated_from": None, "n_actions": A}
 
 
+def cpu_sweep_times_all_cores(*args, **kw):
+    """cpu_sweep_times with BLAS set to every usable CPU (usable_cpus()); the
+    thread count actually in effect is recorded in the result."""
+    usable, aff, quota = usable_cpus()
+    try:
+        from threadpoolctl import threadpool_limits
+        limiter = threadpool_limits(limits=usable, user_api="blas")
+    except Exception:
+        limiter = None
+    try:
+        t = cpu_sweep_times(*args, **kw)
+        t["blas_threads"] = int(blas_threads())
+    finally:
+        if limiter is not None:
+            limiter.restore_original_limits()
+    t.update(usable_cpus=usable, affinity_cpus=aff, cgroup_quota_cpus=quota)
+    return t
+
+
 def cpu_baseline_from(t, k_b, k_f):
     """instance-steps/s of the timed statements at this run's mean sweep counts:
     one step = K_b * t_b + K_f * t_f + t_copy."""
@@ -199,12 +252,18 @@ def cpu_baseline_from(t, k_b, k_f):
         sample = (f"extrapolated: the dense fp64 table does not fit host RAM; per-sweep and copy times "
                   f"measured at {t['extrapolated_from']}x{t['extrapolated_from']} x (S ratio)^2 = "
                   f"{t['ratio']:.0f} -- " + sample)
-    return {"value": 1.0 / t_step, "unit": "instance-steps/s", "cores": int(blas_threads()),
-            "host_cpu_count": os.cpu_count(), "kind": "port", "sample": sample}
+    out = {"value": 1.0 / t_step, "unit": "instance-steps/s", "cores": int(t.get("blas_threads", blas_threads())),
+           "host_cpu_count": os.cpu_count(), "kind": "port", "sample": sample}
+    if "usable_cpus" in t:
+        out.update(usable_cpus=t["usable_cpus"], affinity_cpus=t["affinity_cpus"],
+                   cgroup_quota_cpus=t["cgroup_quota_cpus"],
+                   cores_note=("BLAS threads = the CPUs this process may use: sched_getaffinity capped by the "
+                               "cgroup CPU quota (host_cpu_count is the whole machine)"))
+    return out
 
 
 def cpu_baseline(size, p_slip, k_b, k_f, n_sweeps, causal=False, stay=False):
-    return cpu_baseline_from(cpu_sweep_times(size, p_slip, n_sweeps, causal, stay), k_b, k_f)
+    return cpu_baseline_from(cpu_sweep_times_all_cores(size, p_slip, n_sweeps, causal, stay), k_b, k_f)
 
 
 def config1_timings(device_runs=True):
@@ -309,6 +368,71 @@ def kernel_name(mode, plan, width):
            f"(irlmx::ClusterArgs)"
 
 
+def full_run(args, mdp, e_f, p_0, terminal, causal, dev, barrier, world):
+    """irl to convergence on this rank's instances (maxent.py:236-255: ``while
+    delta > eps``), from theta0 = 1, with converged instances compacted out of
+    the batch (irlmx.batch) unless --no-compact.  Returns the record of rank 0
+    (wall time = the slowest rank's)."""
+    import torch
+    from irlmx import ops
+    from irlmx.batch import BatchedMaxEnt
+    from irlmx.shard import max_over_ranks
+    irl = BatchedMaxEnt(mdp, e_f, p_0, terminal, causal=causal, discount=DISCOUNT if causal else None)
+    B = irl.batch
+    trace = []                       # (step, working batch, seconds, forward sweeps summed over the working set)
+    clock = [time.perf_counter()]
+
+    def on_step(m):
+        torch.cuda.synchronize()
+        now = time.perf_counter()
+        trace.append((m.k, int(m.last_forward_sweeps.gt(0).sum()), now - clock[0],
+                      float(m.last_forward_sweeps.sum())))
+        clock[0] = now
+        if m.k % 200 == 0:
+            print(f"bench.py full run: step {m.k}, {int(m.active.sum())} of {B} instances active", file=sys.stderr,
+                  flush=True)
+
+    ctr0 = ops.counters()
+    torch.cuda.synchronize()
+    barrier()
+    t0 = time.perf_counter()
+    clock[0] = t0
+    _, steps = irl.run(eps=args.full_run_eps, max_steps=args.full_run_max_steps, compact=not args.no_compact,
+                       on_step=on_step)
+    torch.cuda.synchronize()
+    wall = time.perf_counter() - t0
+    wall_max = max_over_ranks(wall, dev)
+    barrier()
+    ctr1 = ops.counters()
+    steps = steps.cpu().numpy()
+    converged = int((~irl.active).sum())
+    work = np.array([w for _, w, _, _ in trace], dtype=np.float64)
+    secs = np.array([t for _, _, t, _ in trace])
+    changes = [(1, int(work[0]))] + [(int(trace[i][0]), int(work[i])) for i in range(1, len(trace))
+                                     if work[i] != work[i - 1]]
+    inst_steps = int(steps.sum())
+    bw = float(np.mean(irl.last_backward_sweeps.cpu().numpy())) if causal else 2.0 * mdp.n_states
+    return {
+        "eps": args.full_run_eps, "compact": not args.no_compact, "instances_per_gpu": B,
+        "instances_total": B * world, "converged_this_rank": converged,
+        "gradient_steps": int(irl.k), "max_steps": args.full_run_max_steps,
+        "steps_per_instance": {"min": int(steps.min()), "median": float(np.median(steps)), "max": int(steps.max()),
+                               "all": [int(v) for v in steps]},
+        "wall_s": wall_max, "instance_steps": inst_steps * world,
+        "instance_steps_per_s": inst_steps * world / wall_max,
+        "irl_runs_per_s": B * world / wall_max,
+        "step1_s": float(secs[0]) if len(secs) else None,
+        "seconds_by_working_batch": {str(int(w)): float(secs[work == w].sum()) for w in np.unique(work)},
+        "working_batch_changes": changes[:64],
+        "forward_sweeps_total": float(sum(f for _, _, _, f in trace)),
+        "backward_sweeps_per_instance_step": bw,
+        "counters": {k: ctr1[k] - ctr0[k] for k in ctr1},
+        "note": ("irl run to max|dtheta| <= eps per instance (maxent.py:240-252) from theta0 = 1 on the bench "
+                 "workload; stopped instances are compacted out of the batch before each step (irlmx.batch), "
+                 "so only active instances pay sweeps; wall = slowest rank, every step synchronised"),
+    }
+
+
 def main(argv=None):
     args = parse(argv)
     # stdout carries exactly one JSON line: whatever libraries print there (gloo's
@@ -379,8 +503,11 @@ def main(argv=None):
            torch.cuda.Event(enable_timing=True)) for _ in range(max(n_all, args.first_steps))]
     sweeps, bsweeps = [], []
 
+    ctr_steps = []   # library event counters (persistent launches, per-sweep reruns) per step
+
     def step(i, timed):
         e0, e1, e2 = ev[i]
+        c0 = ops.counters() if not timed else None
         e0.record(stream)
         pi = irl.backward()
         e1.record(stream)
@@ -389,7 +516,11 @@ def main(argv=None):
         irl.update(svf)
         sweeps.append(iters)
         bsweeps.append(irl.last_backward_sweeps if causal else torch.full_like(iters, 2 * S))
+        if c0 is not None:   # (untimed steps only: the counter read is a host call)
+            c1 = ops.counters()
+            ctr_steps.append((i, {k: c1[k] - c0[k] for k in c0 if c1[k] != c0[k]}))
 
+    ctr_start = ops.counters()
     elapsed, per_step = timed_steps(step, args.steps, args.warmup, barrier, torch.cuda.synchronize)
     elapsed_max = max_over_ranks(elapsed, dev)
     value, ms_per_step = headline(elapsed_max, per_gpu, world, args.steps)
@@ -402,6 +533,7 @@ def main(argv=None):
         torch.cuda.synchronize()
         per_step.append(time.perf_counter() - t)
 
+    ctr_end = ops.counters()
     k_f_all = torch.stack(sweeps).to(torch.float64).cpu().numpy()      # [steps run, B]
     k_b_all = torch.stack(bsweeps).to(torch.float64).cpu().numpy()
     timed = slice(args.warmup, n_all)
@@ -480,16 +612,28 @@ def main(argv=None):
         }
         if n_first:
             t_first = sum(per_step[:n_first])
+            bwd_ms = [ev[i][0].elapsed_time(ev[i][1]) for i in range(n_first)]
+            fwd_ms = [ev[i][1].elapsed_time(ev[i][2]) for i in range(n_first)]
             out["first_steps"] = {
                 "steps": n_first, "seconds": t_first, "instance_steps_per_s": per_gpu * n_first / t_first,
                 "step1_ms": per_step[0] * 1e3,
+                # step 1's phases (HIP events on the launch stream): backward, forward to convergence
+                # from the unit reward, and the rest (gradient, update, host work) = step1_ms - both
+                "step1_backward_ms": bwd_ms[0], "step1_forward_ms": fwd_ms[0],
+                "step1_other_ms": per_step[0] * 1e3 - bwd_ms[0] - fwd_ms[0],
+                "step1_forward_us_per_sweep": fwd_ms[0] * 1e3 / max(1.0, float(k_f_all[0].max())),
+                "backward_ms": [round(v, 3) for v in bwd_ms], "forward_ms": [round(v, 3) for v in fwd_ms],
+                # per untimed step: library events that occurred (persistent launches, per-sweep reruns
+                # after a non-finite value, a failed co-residency rendezvous or an exchange timeout)
+                "events": {str(i + 1): c for i, c in ctr_steps if i < n_first},
                 "forward_sweeps_mean": [float(v) for v in k_f_all[:n_first].mean(axis=1)],
                 "note": ("steps 1..N of irl from theta0 = 1 on this GPU's instances, each timed to its own sync "
                          "(the warm-up and timed steps are the first W + K); step 1's forward runs to convergence "
                          "from the unit reward (~360k sweeps at 128x128)")}
+        out["counters"] = {k: ctr_end[k] - ctr_start[k] for k in ctr_end}
         out["roofline"]["stream_copy_GBs"] = stream_copy_gbs(dev)
         if world == 1 and not args.no_cpu_baseline:
-            t = cpu_sweep_times(size, float(slips[0]), args.cpu_sweeps, causal, stay)
+            t = cpu_sweep_times_all_cores(size, float(slips[0]), args.cpu_sweeps, causal, stay)
             out["cpu_baseline"] = cpu_baseline_from(t, float(k_b.mean()), float(k_f.mean()))
             out["speedup_vs_cpu"] = out["value"] / out["cpu_baseline"]["value"]
             if n_first:
@@ -500,6 +644,18 @@ def main(argv=None):
                 out["first_steps"]["speedup_vs_cpu"] = out["first_steps"]["instance_steps_per_s"] * t_cpu / n_first
             if not args.no_config1:
                 out["config1"] = config1_timings()
+    if args.full_run:
+        fr = full_run(args, mdp, e_f, p_0, terminal, causal, dev, barrier, world)
+        if rank == 0:
+            if "cpu_baseline" in out:
+                # the reference's statements for the same run: every instance-step pays K_b backward
+                # sweeps and one call's copies, plus the forward sweeps it logged
+                t_cpu = fr["instance_steps"] * (fr["backward_sweeps_per_instance_step"] * t["t_b"] + t["t_copy"]) \
+                    + fr["forward_sweeps_total"] * t["t_f"]
+                fr["cpu_baseline_s"] = t_cpu
+                fr["speedup_vs_cpu"] = t_cpu / fr["wall_s"]
+            out["full_run"] = fr
+    if rank == 0:
         print(json.dumps(out), file=json_out, flush=True)
     if world > 1:
         dist.destroy_process_group()

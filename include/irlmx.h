@@ -97,6 +97,21 @@ typedef struct irlmx_mdp {
 int irlmx_abi_version(void);
 const char* irlmx_last_error(void);
 
+/*
+ * Process-wide event counters (diagnostics; no reference counterpart): how often
+ * the persistent shapes ran and how often a call was rerun on the per-sweep
+ * shape.  Copies min(n, IRLMX_COUNTERS_LEN) counters into out (host memory) and
+ * returns IRLMX_COUNTERS_LEN.  Counts only grow; callers take differences.
+ */
+#define IRLMX_COUNTERS_LEN 6
+#define IRLMX_CTR_CLUSTER_LAUNCHES 0   /* persistent cluster launches (stencil forward / backward) */
+#define IRLMX_CTR_GRID_LAUNCHES 1      /* persistent grid launches (soft VI / VI / ELL passes) */
+#define IRLMX_CTR_RERUN_NONFINITE 2    /* cluster forward saw a non-finite value: rerun per sweep (exact NaN rules) */
+#define IRLMX_CTR_RERUN_NOT_RESIDENT 3 /* workgroups could not all run at once: rerun per sweep */
+#define IRLMX_CTR_RERUN_TIMEOUT 4      /* a halo / value exchange timed out (a descheduled workgroup): rerun per sweep */
+#define IRLMX_CTR_SWEEP_CALLS 5        /* calls (or reruns) that took the per-sweep shape */
+int irlmx_counters(int64_t* out, int32_t n);
+
 /* Bytes of device workspace `op` needs for this model (0 is a valid answer). */
 size_t irlmx_workspace_bytes(const irlmx_mdp* mdp, int32_t op);
 
@@ -157,6 +172,7 @@ int irlmx_value_iteration(const irlmx_mdp* mdp, const double* reward, double dis
  *   [6] in-tile layout (0 per state, 1 pair rows, 2 column pairs, 3 column quads)
  *   [7] threads per workgroup  [8] sequential launches   [9] LDS bytes
  * Cluster fields are 0 for the other shapes.  Depends on the current device.
+ * A backward plan assumes rescale != 0 unless op carries IRLMX_PLAN_NO_RESCALE.
  */
 #define IRLMX_PLAN_LEN 10
 #define IRLMX_SHAPE_FUSED 0   /* one workgroup per instance for the whole loop */
@@ -166,6 +182,8 @@ int irlmx_value_iteration(const irlmx_mdp* mdp, const double* reward, double dis
 #define IRLMX_SHAPE_DENSE_GEMM 4 /* DENSE, shared table: the backward sweep as one dgemm over all instances */
 #define IRLMX_SHAPE_GRID 5    /* soft VI / VI on large grids: one persistent launch, values exchanged per sweep
                                  ([3] = workgroups per instance) */
+#define IRLMX_PLAN_NO_RESCALE 0x100 /* OR into op (IRLMX_OP_BACKWARD only): the plan of a rescale = 0 call, which
+                                      never takes the cluster shape (its overflow bookkeeping is per sweep) */
 int irlmx_execution_plan(const irlmx_mdp* mdp, int32_t op, int64_t* plan);
 
 /*
@@ -203,6 +221,15 @@ int irlmx_dense_to_stencil(const double* dense, int32_t width, int32_t height, i
                            double* row_val, int32_t* off_stencil, void* stream);
 
 /*
+ * Dense [S][S][A] float64 table (device, the reference's p_transition layout)
+ * -> DENSE layout: p_rows [A][S][S] (P[s, t, a] at [a][s][t]) and m_rows [S][S]
+ * (sum over actions in action order).  Replaces the per-call slice copies of
+ * maxent.py:98-102, 143, 320 and solver.py:37 for genuinely dense models.
+ */
+int irlmx_dense_to_rows(const double* dense, int32_t n_states, int32_t n_actions, double* p_rows, double* m_rows,
+                        void* stream);
+
+/*
  * Dense [S][S][A] float64 table (device) -> ELL layout (any sparsity), in two
  * calls.  irlmx_dense_ell_sizes writes k_out[0] = max targets per source state
  * (union over actions) and k_out[1] = max sources per target state (device
@@ -214,19 +241,24 @@ int irlmx_dense_to_stencil(const double* dense, int32_t width, int32_t height, i
  * conversion of the reference's dense p_transition (maxent.py:98-102, 143) for
  * non-grid models.
  */
-/*
- * Dense [S][S][A] float64 table (device, the reference's p_transition layout)
- * -> DENSE layout: p_rows [A][S][S] (P[s, t, a] at [a][s][t]) and m_rows [S][S]
- * (sum over actions in action order).  Replaces the per-call slice copies of
- * maxent.py:98-102, 143, 320 and solver.py:37 for genuinely dense models.
- */
-int irlmx_dense_to_rows(const double* dense, int32_t n_states, int32_t n_actions, double* p_rows, double* m_rows,
-                        void* stream);
-
 int irlmx_dense_ell_sizes(const double* dense, int32_t n_states, int32_t n_actions, int32_t* k_out,
                           int32_t* col_count, void* stream);
 int irlmx_dense_to_ell(const double* dense, int32_t n_states, int32_t n_actions, int32_t k_row, int32_t k_col,
                        int32_t* row_idx, double* row_val, int32_t* col_idx, double* col_val, void* stream);
+
+/*
+ * Batched fp64 GEMM on the matrix cores (v_mfma_f64_16x16x4_f64): c[b][r] =
+ * sum_t m[r][t] * z[b][t] for m [rows][n], z [batch][n], c [batch][rows], all
+ * row-major device arrays.  This is the P . [v_1 .. v_B] contraction of a dense
+ * table shared by B instances (maxent.py:155, 329; solver.py:44), which the
+ * DENSE-layout passes run through it (plan shape IRLMX_SHAPE_DENSE_GEMM); any n
+ * (the K tail is zero-padded).  irlmx_dense_gemm_variant reports the kernel
+ * variant such a call launches: variant[4] = {row tiles of 16 per workgroup,
+ * instance tiles of 16, waves per workgroup, 16-byte loads (n even)}.
+ */
+int irlmx_dense_gemm(const double* m, const double* z, double* c, int32_t rows, int32_t n, int32_t batch,
+                     void* stream);
+int irlmx_dense_gemm_variant(int32_t rows, int32_t n, int32_t batch, int32_t* variant);
 
 #ifdef __cplusplus
 }

@@ -3,6 +3,7 @@
 
 #include <hip/hip_runtime.h>
 
+#include <atomic>
 #include <cstdarg>
 #include <cstdio>
 
@@ -24,8 +25,21 @@ int hip_fail(hipError_t e, const char* what) {
   return IRLMX_EHIP;
 }
 
+static std::atomic<long long> g_counters[IRLMX_COUNTERS_LEN];
+
+void count_event(int which) {
+  if (which >= 0 && which < IRLMX_COUNTERS_LEN) g_counters[which].fetch_add(1, std::memory_order_relaxed);
+}
+
 }  // namespace irlmx
 
 extern "C" int irlmx_abi_version(void) { return IRLMX_ABI_VERSION; }
 
 extern "C" const char* irlmx_last_error(void) { return irlmx::g_err; }
+
+extern "C" int irlmx_counters(int64_t* out, int32_t n) {
+  if (out)
+    for (int i = 0; i < n && i < IRLMX_COUNTERS_LEN; ++i)
+      out[i] = irlmx::g_counters[i].load(std::memory_order_relaxed);
+  return IRLMX_COUNTERS_LEN;
+}

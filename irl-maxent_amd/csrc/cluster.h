@@ -47,6 +47,8 @@ struct ClusterArgs {
   unsigned salt;           // per-launch granule tag salt
   int* err;                // [0]: exchange timeout (1), non-finite (2), not co-resident (4); [1..2]: rendezvous
   int n_resident;          // workgroups of this launch that must run at once (coresident())
+  unsigned long long gather_ticks;  // exchange timeout (s_memrealtime ticks; kGatherTicks unless a test shortens it)
+  int test_drop;           // tests only (IRLMX_TEST_DROP_TILE): this workgroup leaves after the rendezvous, else -1
   unsigned long long* stamps;  // optional [grid][8] phase cycle counters (IRLMX_STAMPS=1), else null
   double* out;             // forward: svf [B][S]; backward: pi [B][S][A]
   int64_t* iters;
@@ -86,10 +88,13 @@ __device__ inline void gran_store(__amdgpu_buffer_rsrc_t r, unsigned off, unsign
 }
 // Poll the granule pairs selected by `want` (bit k: entry k; the last entry
 // through rsrc `rl`, the others through `r`) until all carry `tag`; false
-// after 20 s.  Every pending load of a pass is in flight at once.
+// after `limit` ticks of s_memrealtime (100 MHz; default 20 s).  Every pending
+// load of a pass is in flight at once.
+constexpr unsigned long long kGatherTicks = 2000000000ull;
 template <int N>
 __device__ inline bool gran_gather(__amdgpu_buffer_rsrc_t r, __amdgpu_buffer_rsrc_t rl, const unsigned (&off)[N],
-                                   unsigned want, unsigned tag, unsigned long long (&v)[N]) {
+                                   unsigned want, unsigned tag, unsigned long long (&v)[N],
+                                   unsigned long long limit = kGatherTicks) {
   unsigned pending = want;
   const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
   while (pending) {
@@ -105,7 +110,7 @@ __device__ inline bool gran_gather(__amdgpu_buffer_rsrc_t r, __amdgpu_buffer_rsr
         pending &= ~(1u << k);
       }
     if (!pending) break;
-    if (__builtin_amdgcn_s_memrealtime() - t0 > 2000000000ull) return false;
+    if (__builtin_amdgcn_s_memrealtime() - t0 > limit) return false;
     __builtin_amdgcn_s_sleep(IRLMX_POLL_SLEEP);
   }
   return true;

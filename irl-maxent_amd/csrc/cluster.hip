@@ -138,6 +138,7 @@ __global__ void __launch_bounds__(NT) cluster_kernel(ClusterArgs a) {
       return;
     }
   }
+  if (lin == a.test_drop) return;  // tests: a workgroup that stops publishing (exchange-timeout path)
   const int r0 = tile * a.R, r1 = min(H, r0 + a.R);
   const int e0 = max(0, r0 - a.G), e1 = min(H, r1 + a.G);
   const int E = (e1 - e0) * W;
@@ -478,7 +479,7 @@ __global__ void __launch_bounds__(NT) cluster_kernel(ClusterArgs a) {
       for (int t0 = 0; t0 < a.C; t0 += kWave) {
         unsigned long long v[1] = {xcc};
         unsigned off[1] = {(2u * (unsigned)a.H + (unsigned)(t0 + tid)) * 16u};
-        ok &= gran_gather<1>(rs, rs, off, t0 + tid < a.C ? 1u : 0u, htag, v);
+        ok &= gran_gather<1>(rs, rs, off, t0 + tid < a.C ? 1u : 0u, htag, v, a.gather_ticks);
         diff |= v[0] ^ xcc;
       }
       diff = wave_or_u64(diff);
@@ -672,7 +673,7 @@ __global__ void __launch_bounds__(NT) cluster_kernel(ClusterArgs a) {
         off[GPT] = ((unsigned)(m & 1) * (unsigned)a.H + (unsigned)tid) * 16u;
         want |= (k0 == 0 && tid < a.C ? 1u : 0u) << GPT;
         unsigned long long v[GPT + 1];
-        ok &= gran_gather<GPT + 1>(rg, rs, off, want, tag, v);
+        ok &= gran_gather<GPT + 1>(rg, rs, off, want, tag, v, a.gather_ticks);
 #pragma unroll
         for (int i = 0; i < GPT; ++i)
           if ((want >> i) & 1u) cur[pad + ls[i]] = bits_double(v[i]);
@@ -838,10 +839,19 @@ static int device_cus() {
   return cus;
 }
 
+// CUs the planner plans for: the device's, or IRLMX_PLAN_CUS (tests: a planner
+// that believes in more CUs than exist produces a grid that cannot be
+// co-resident, which cluster_run must reject; the host-side sanitizer build
+// plans without a device).  The co-residency check always uses device_cus().
+static int plan_cus() {
+  const int forced = env_int("IRLMX_PLAN_CUS", 0);
+  return forced > 0 ? forced : device_cus();
+}
+
 // Can the C tiles of each of nb instances sit in one XCD group (<= CUs / 8
 // workgroups per group, one per CU)?
 static bool xcd_groupable(int nb, int C) {
-  const int cus = device_cus();
+  const int cus = plan_cus();
   return cus >= 8 && ((nb + 7) / 8) * C <= cus / 8;
 }
 
@@ -864,7 +874,7 @@ static size_t cluster_lds(int emax, int W, int layout, int nt, int mode) {
 // smallest extended tile.  IRLMX_CLUSTER_R / _G force a plan (tests).
 bool cluster_plan(int W, int H, int B, int mode, ClusterPlan* out) {
   if (env_int("IRLMX_CLUSTER", 1) == 0) return false;
-  const int cus = device_cus();
+  const int cus = plan_cus();
   if (cus <= 0) return false;
   const int fR = env_int("IRLMX_CLUSTER_R", 0), fG = env_int("IRLMX_CLUSTER_G", 0);
   // in-tile layout (IRLMX_PAIR forces one): widths 64 / 128 column pairs (2;
@@ -1017,6 +1027,12 @@ int cluster_run(int mode, const ClusterPlan& plan, ClusterArgs a, int B, hipStre
   // IRLMX_TEST_NOT_RESIDENT=1 (tests only): wait for one workgroup more than
   // the launch has, i.e. take the not-co-resident path deterministically
   const int extra = env_int("IRLMX_TEST_NOT_RESIDENT", 0) ? 1 : 0;
+  // IRLMX_TEST_DROP_TILE=<workgroup> and IRLMX_TEST_EXCHANGE_TIMEOUT_MS=<ms> (tests
+  // only): one workgroup leaves after the rendezvous, so its neighbours' exchange
+  // times out (after the shortened limit) and the call takes the rerun path
+  a.test_drop = env_int("IRLMX_TEST_DROP_TILE", -1);
+  const int tmo_ms = env_int("IRLMX_TEST_EXCHANGE_TIMEOUT_MS", 0);
+  a.gather_ticks = tmo_ms > 0 ? (unsigned long long)tmo_ms * 100000ull : kGatherTicks;
   for (int b0 = 0; b0 < B; b0 += p.per_launch) {
     const int nb = std::min(p.per_launch, B - b0);
     a.b0 = b0;
@@ -1032,6 +1048,7 @@ int cluster_run(int mode, const ClusterPlan& plan, ClusterArgs a, int B, hipStre
     const int grid = a.xcd_group ? 8 * ((nb + 7) / 8) * p.C : nb * p.C;
     e = hipLaunchKernel(fn, dim3(grid), dim3(nt), args, p.lds, st);
     if (e != hipSuccess) return hip_fail(e, "cluster launch");
+    count_event(IRLMX_CTR_CLUSTER_LAUNCHES);
   }
   int err = 0;
   e = hipMemcpyAsync(&err, a.err, sizeof(int), hipMemcpyDeviceToHost, st);
@@ -1061,8 +1078,24 @@ int cluster_run(int mode, const ClusterPlan& plan, ClusterArgs a, int B, hipStre
     free(h);
     (void)hipFree(stamps);
   }
-  if (err & kErrNotResident) return kClusterNotResident;
-  if (err & 1) { set_error("cluster: halo exchange timed out (workgroups not co-resident?)"); return IRLMX_EHIP; }
+  if (err & kErrNotResident) {
+    count_event(IRLMX_CTR_RERUN_NOT_RESIDENT);
+    return kClusterNotResident;
+  }
+  // A halo exchange that timed out (20 s): every workgroup passed the rendezvous,
+  // but one was descheduled later (e.g. compute-wave save/restore on a GPU shared
+  // with another process) and its neighbours gave up waiting for its granules.
+  // The call is rerun on the per-sweep shape like a failed rendezvous, so a
+  // caller on a shared GPU still gets the same answers; the counter records it.
+  // IRLMX_STRICT_EXCHANGE=1 reports it as an error instead (tests).
+  if (err & 1) {
+    if (env_int("IRLMX_STRICT_EXCHANGE", 0)) {
+      set_error("cluster: halo exchange timed out (workgroups not co-resident?)");
+      return IRLMX_EHIP;
+    }
+    count_event(IRLMX_CTR_RERUN_TIMEOUT);
+    return kClusterNotResident;
+  }
   return (err & 2) ? kClusterNonFinite : 0;
 }
 

@@ -12,6 +12,8 @@ namespace irlmx {
 constexpr int kWave = 64;
 constexpr int kStencilK = 5;  // self, +x, -x, +y, -y
 
+void count_event(int which);  // irlmx_counters (capi.hip): IRLMX_CTR_*
+
 // Direction k of the 5-point stencil, in the reference's action order
 // (gridworld.py:47: (1,0), (-1,0), (0,1), (0,-1)); k = 0 is "stay".
 __host__ __device__ inline int stencil_opposite(int k) {

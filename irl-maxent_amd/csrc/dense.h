@@ -90,10 +90,12 @@ void dense_bellman_sweep_launch(const DenseView& d, const DenseBellman& a, Dense
                                 hipStream_t st);
 void dense_bellman_finish_launch(const DenseView& d, const DenseBellman& a, DenseBufs w, hipStream_t st);
 // shared table: the sweep's A products P_a . [v_1 .. v_B] on the MFMA kernel (w.wt = [B][A][S]) + the update
-void dense_bellman_gemm_sweep_launch(const DenseView& d, const DenseBellman& a, DenseBufs w, long long it, int r3,
-                                     hipStream_t st);
-// C[b][r] = sum_t M[r][t] Z[b][t], M [R][S], Z [B][S], on the fp64 matrix cores (needs S % 4 == 0)
-bool dense_gemm_mfma_ok(int S);
-void dense_gemm_launch(const double* M, const double* Z, double* C, int R, int S, int B, hipStream_t st);
+hipError_t dense_bellman_gemm_sweep_launch(const DenseView& d, const DenseBellman& a, DenseBufs w, long long it,
+                                           int r3, hipStream_t st);
+// C[b][r] = sum_t M[r][t] Z[b][t], M [R][S], Z [B][S], on the fp64 matrix cores (any S; rows of M and Z
+// contiguous); returns the attribute / launch error, if any
+hipError_t dense_gemm_launch(const double* M, const double* Z, double* C, int R, int S, int B, hipStream_t st);
+// {ST row tiles, NBT instance tiles, waves, 16-byte loads} of the launch dense_gemm_launch makes
+void dense_gemm_variant(int R, int S, int B, int* out);
 
 }  // namespace irlmx

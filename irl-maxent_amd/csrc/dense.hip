@@ -21,6 +21,8 @@
 
 #include <hip/hip_runtime.h>
 
+#include <atomic>
+
 #include "dense.h"
 
 namespace irlmx {
@@ -433,11 +435,16 @@ dense_bellman_finish_kernel(DenseView d, DenseBellman a, DenseBufs w) {
 // four lanes of a column), and MFMA x (x = 0..3) uses element x of them: the
 // k index of both operands maps to the same t = 16 c + 4 (l >> 4) + x.  M is
 // read from HBM once per sweep; Z (B x S) is re-read per 32 rows of M (L2).
+//
+// Any S: the K tail (S % 16 != 0) is zero-padded per element -- a padded term
+// is 0 * 0, exactly 0, so the sums are those of the unpadded products -- and
+// rows start 16-byte aligned only when S is even (V2: two 16-byte loads per
+// operand row and chunk), else the kernel loads doubles one by one.
 typedef double f64x4 __attribute__((ext_vector_type(4)));
 
 // ST 16-row tiles of M and NBT 16-instance column tiles per workgroup (sized to
 // S and B so that the grid fills the chip)
-template <int ST, int NBT, int kGemmWaves>
+template <int ST, int NBT, int kGemmWaves, bool V2>
 __global__ void __launch_bounds__(kGemmWaves * kWave)
 dense_gemm_kernel(const double* __restrict__ M, const double* __restrict__ Z, double* __restrict__ C, int R, int S,
                   int B) {  // M [R][S], Z [B][S] -> C [B][R]
@@ -468,27 +475,32 @@ dense_gemm_kernel(const double* __restrict__ M, const double* __restrict__ Z, do
     zok[bt] = r < B;
     zrow[bt] = Z + (size_t)(zok[bt] ? r : 0) * S;
   }
-  // the 4 consecutive t of chunk c this lane supplies (S % 4 == 0: all in or all out)
+  // the 4 consecutive t of chunk c this lane supplies, zero beyond S
+  auto load4 = [&](const double* row, int t, bool ok, double2 (&o)[2]) {
+    o[0] = o[1] = make_double2(0.0, 0.0);
+    if (!ok || t >= S) return;
+    if (t + 3 < S) {
+      if constexpr (V2) {
+        o[0] = *reinterpret_cast<const double2*>(row + t);
+        o[1] = *reinterpret_cast<const double2*>(row + t + 2);
+      } else {
+        o[0] = make_double2(row[t], row[t + 1]);
+        o[1] = make_double2(row[t + 2], row[t + 3]);
+      }
+    } else {  // the K tail
+      o[0].x = row[t];
+      if (t + 1 < S) o[0].y = row[t + 1];
+      if (t + 2 < S) o[1].x = row[t + 2];
+    }
+  };
   double2 ma[ST][2], za[NBT][2];
   auto load = [&](int c, double2 (&mo)[ST][2], double2 (&zo)[NBT][2]) {
     const int t = 16 * c + 4 * q;
-    const bool tok = c < c1 && t < S;
+    const bool tok = c < c1;
 #pragma unroll
-    for (int st = 0; st < ST; ++st) {
-      mo[st][0] = mo[st][1] = make_double2(0.0, 0.0);
-      if (tok && mok[st]) {
-        mo[st][0] = *reinterpret_cast<const double2*>(mrow[st] + t);
-        mo[st][1] = *reinterpret_cast<const double2*>(mrow[st] + t + 2);
-      }
-    }
+    for (int st = 0; st < ST; ++st) load4(mrow[st], t, tok && mok[st], mo[st]);
 #pragma unroll
-    for (int bt = 0; bt < NBT; ++bt) {
-      zo[bt][0] = zo[bt][1] = make_double2(0.0, 0.0);
-      if (tok && zok[bt]) {
-        zo[bt][0] = *reinterpret_cast<const double2*>(zrow[bt] + t);
-        zo[bt][1] = *reinterpret_cast<const double2*>(zrow[bt] + t + 2);
-      }
-    }
+    for (int bt = 0; bt < NBT; ++bt) load4(zrow[bt], t, tok && zok[bt], zo[bt]);
   };
   auto el = [](const double2 (&v)[2], int x) { return x == 0 ? v[0].x : x == 1 ? v[0].y : x == 2 ? v[1].x : v[1].y; };
   load(c0, ma, za);
@@ -532,8 +544,29 @@ dense_gemm_kernel(const double* __restrict__ M, const double* __restrict__ Z, do
 
 namespace {
 dim3 row_grid(const DenseView& d) { return dim3((d.S + kDenseRowsPerBlock - 1) / kDenseRowsPerBlock, d.B); }
-bool lds_vec(const DenseView& d) { return dense_lds_vec(d); }
 size_t lds_bytes(int S) { return (size_t)S * sizeof(double); }
+
+// The LDS-staged kernels take up to kDenseLdsMaxStates doubles (64 KiB) of dynamic
+// LDS on top of their static words: beyond the default limit, so the attribute is
+// raised once per device before the first staged launch.  A failure here leaves
+// the launch to fail, which the callers' hipGetLastError checks report.
+void lds_prep() {
+  static std::atomic<int> done[64];
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64 || done[dev].load(std::memory_order_acquire)) return;
+  const int bytes = (int)(kDenseLdsMaxStates * sizeof(double));
+  for (const void* fn : {(const void*)&dense_fwd_sweep_kernel<true>, (const void*)&dense_bwd_sweep_kernel<true>,
+                         (const void*)&dense_bwd_final_kernel<true>, (const void*)&dense_bellman_sweep_kernel<true>,
+                         (const void*)&dense_bellman_finish_kernel<true>})
+    (void)hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, bytes);
+  done[dev].store(1, std::memory_order_release);
+}
+
+bool lds_vec(const DenseView& d) {
+  const bool v = dense_lds_vec(d);
+  if (v) lds_prep();
+  return v;
+}
 }  // namespace
 
 void dense_rows_launch(const double* dense, int S, int A, double* P, double* M, hipStream_t st) {
@@ -599,13 +632,14 @@ void dense_bellman_sweep_launch(const DenseView& d, const DenseBellman& a, Dense
     hipLaunchKernelGGL(dense_bellman_sweep_kernel<false>, row_grid(d), dim3(kDenseThreads), 0, st, d, a, w, it, r3);
 }
 
-void dense_bellman_gemm_sweep_launch(const DenseView& d, const DenseBellman& a, DenseBufs w, long long it, int r3,
-                                     hipStream_t st) {
+hipError_t dense_bellman_gemm_sweep_launch(const DenseView& d, const DenseBellman& a, DenseBufs w, long long it,
+                                           int r3, hipStream_t st) {
   const double* vin = (it & 1) ? w.buf1 : w.buf0;
   // all actions in one GEMM: the stacked P [A * S][S] times [v_1 .. v_B] -> c[b][a * S + s]
-  dense_gemm_launch(d.P, vin, w.wt, d.A * d.S, d.S, d.B, st);
+  if (hipError_t e = dense_gemm_launch(d.P, vin, w.wt, d.A * d.S, d.S, d.B, st)) return e;
   hipLaunchKernelGGL(dense_bellman_gemm_epilogue_kernel, dim3((d.S + kDenseThreads - 1) / kDenseThreads, d.B),
                      dim3(kDenseThreads), 0, st, d, a, w, w.wt, it, r3);
+  return hipGetLastError();
 }
 
 void dense_bellman_finish_launch(const DenseView& d, const DenseBellman& a, DenseBufs w, hipStream_t st) {
@@ -620,40 +654,55 @@ void dense_bellman_finish_launch(const DenseView& d, const DenseBellman& a, Dens
 
 namespace irlmx {
 
-bool dense_gemm_mfma_ok(int S) { return S % 4 == 0; }
-
 bool dense_lds_vec(const DenseView& d) { return d.S <= kDenseLdsMaxStates && d.B > 1; }
 
 template <int ST, int NBT, int NW>
-static void gemm_go(const double* M, const double* Z, double* C, int R, int S, int B, hipStream_t st) {
-  const size_t lds = (size_t)NW * ST * NBT * 4 * kWave * sizeof(double);
-  (void)hipFuncSetAttribute((const void*)&dense_gemm_kernel<ST, NBT, NW>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                            (int)lds);
+static hipError_t gemm_go(const double* M, const double* Z, double* C, int R, int S, int B, hipStream_t st) {
+  const size_t lds = (size_t)NW * ST * NBT * 4 * kWave * sizeof(double);  // up to 128 KiB (ST 2, NBT 4, 8 waves)
+  const void* fn = (S % 2 == 0) ? (const void*)&dense_gemm_kernel<ST, NBT, NW, true>
+                                : (const void*)&dense_gemm_kernel<ST, NBT, NW, false>;
+  hipError_t e = hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+  if (e != hipSuccess) return e;
   const dim3 grid((R + 16 * ST - 1) / (16 * ST), (B + 16 * NBT - 1) / (16 * NBT));
-  hipLaunchKernelGGL((dense_gemm_kernel<ST, NBT, NW>), grid, dim3(NW * kWave), lds, st, M, Z, C, R, S, B);
+  if (S % 2 == 0)
+    hipLaunchKernelGGL((dense_gemm_kernel<ST, NBT, NW, true>), grid, dim3(NW * kWave), lds, st, M, Z, C, R, S, B);
+  else
+    hipLaunchKernelGGL((dense_gemm_kernel<ST, NBT, NW, false>), grid, dim3(NW * kWave), lds, st, M, Z, C, R, S, B);
+  return hipGetLastError();
 }
 
 template <int ST, int NBT>
-static void gemm_waves(const double* M, const double* Z, double* C, int R, int S, int B, hipStream_t st) {
+static hipError_t gemm_waves(const double* M, const double* Z, double* C, int R, int S, int B, hipStream_t st) {
   const long long wgs = (long long)((R + 16 * ST - 1) / (16 * ST)) * ((B + 16 * NBT - 1) / (16 * NBT));
-  if (wgs >= 512) gemm_go<ST, NBT, 4>(M, Z, C, R, S, B, st);  // several workgroups per CU
-  else gemm_go<ST, NBT, 8>(M, Z, C, R, S, B, st);
+  if (wgs >= 512) return gemm_go<ST, NBT, 4>(M, Z, C, R, S, B, st);  // several workgroups per CU
+  return gemm_go<ST, NBT, 8>(M, Z, C, R, S, B, st);
 }
 
-void dense_gemm_launch(const double* M, const double* Z, double* C, int R, int S, int B, hipStream_t st) {
+hipError_t dense_gemm_launch(const double* M, const double* Z, double* C, int R, int S, int B, hipStream_t st) {
   const int nbt = B <= 16 ? 1 : (B <= 32 ? 2 : 4);
   const int ny = (B + 16 * nbt - 1) / (16 * nbt);
   // two row tiles per wave (half the Z re-reads) while that still gives >= 256 workgroups
   const bool st2 = (long long)((R + 31) / 32) * ny >= 256;
   if (st2) {
-    if (nbt == 1) gemm_waves<2, 1>(M, Z, C, R, S, B, st);
-    else if (nbt == 2) gemm_waves<2, 2>(M, Z, C, R, S, B, st);
-    else gemm_waves<2, 4>(M, Z, C, R, S, B, st);
-  } else {
-    if (nbt == 1) gemm_waves<1, 1>(M, Z, C, R, S, B, st);
-    else if (nbt == 2) gemm_waves<1, 2>(M, Z, C, R, S, B, st);
-    else gemm_waves<1, 4>(M, Z, C, R, S, B, st);
+    if (nbt == 1) return gemm_waves<2, 1>(M, Z, C, R, S, B, st);
+    if (nbt == 2) return gemm_waves<2, 2>(M, Z, C, R, S, B, st);
+    return gemm_waves<2, 4>(M, Z, C, R, S, B, st);
   }
+  if (nbt == 1) return gemm_waves<1, 1>(M, Z, C, R, S, B, st);
+  if (nbt == 2) return gemm_waves<1, 2>(M, Z, C, R, S, B, st);
+  return gemm_waves<1, 4>(M, Z, C, R, S, B, st);
+}
+
+// the kernel variant a launch of these sizes runs: {ST, NBT, waves, V2}
+void dense_gemm_variant(int R, int S, int B, int* out) {
+  const int nbt = B <= 16 ? 1 : (B <= 32 ? 2 : 4);
+  const int ny = (B + 16 * nbt - 1) / (16 * nbt);
+  const int st = (long long)((R + 31) / 32) * ny >= 256 ? 2 : 1;
+  const long long wgs = (long long)((R + 16 * st - 1) / (16 * st)) * ny;
+  out[0] = st;
+  out[1] = nbt;
+  out[2] = wgs >= 512 ? 4 : 8;
+  out[3] = S % 2 == 0 ? 1 : 0;
 }
 
 }  // namespace irlmx

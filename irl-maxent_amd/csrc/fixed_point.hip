@@ -31,9 +31,8 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <initializer_list>
 #include <vector>
-
-#include <rocblas/rocblas.h>
 
 #include "cluster.h"
 #include "common.h"
@@ -1278,6 +1277,11 @@ static void* grid_fn(const Model& m, int op, int spt) {
 }
 
 static int grid_capacity(void* fn) {
+  // IRLMX_PLAN_CUS x IRLMX_PLAN_GRID_PER_CU: planning without a device (the
+  // host-side sanitizer build, tools/sanitize); a launch always re-checks
+  // co-residency on the device (coresident()), so a wrong figure cannot hang
+  const int f_cus = getenv_int("IRLMX_PLAN_CUS", 0), f_per = getenv_int("IRLMX_PLAN_GRID_PER_CU", 0);
+  if (f_cus > 0 && f_per > 0) return f_cus * f_per;
   int dev = 0, cus = 0, per_cu = 0;
   if (hipGetDevice(&dev) != hipSuccess) return 0;
   if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess) return 0;
@@ -1325,16 +1329,24 @@ static int grid_launch(const Model& m, int op, const GridPlan& gp, void** args, 
   const int grid = gp.xcd ? 8 * ((m.B + 7) / 8) * gp.bpi : gp.bpi * m.B;
   hipError_t e = hipLaunchKernel(grid_fn(m, op, gp.spt), dim3(grid), dim3(kGridThreads), args, 0, st);
   if (e != hipSuccess) return hip_fail(e, "grid launch");
+  count_event(IRLMX_CTR_GRID_LAUNCHES);
   int err = 0;
   e = hipMemcpyAsync(&err, ws.err, sizeof(int), hipMemcpyDeviceToHost, st);
   if (e == hipSuccess) e = hipStreamSynchronize(st);
   if (e != hipSuccess) return hip_fail(e, "grid sync");
-  if (err & kErrNotResident) {
-    // not all workgroups could run at once: clear the words for the per-sweep rerun
+  // not all workgroups could run at once, or (after a passed rendezvous) one was
+  // descheduled long enough for an exchange to time out: clear the words and
+  // rerun on the per-sweep shape (cluster_run treats both cases the same way)
+  const bool timeout = err && !(err & kErrNotResident);
+  if (timeout && getenv_int("IRLMX_STRICT_EXCHANGE", 0)) {
+    set_error("grid shape: exchange timed out (workgroups not co-resident?)");
+    return IRLMX_EHIP;
+  }
+  if (err) {
+    count_event(timeout ? IRLMX_CTR_RERUN_TIMEOUT : IRLMX_CTR_RERUN_NOT_RESIDENT);
     e = hipMemsetAsync(ws.err, 0, 4 * sizeof(int), st);
     return e == hipSuccess ? kClusterNotResident : hip_fail(e, "grid err reset");
   }
-  if (err) { set_error("grid shape: exchange timed out (workgroups not co-resident?)"); return IRLMX_EHIP; }
   return 0;
 }
 
@@ -1456,9 +1468,13 @@ static int validate(const irlmx_mdp* mdp) {
   if (m.A > kMaxActions) { set_error("n_actions=%d exceeds %d", m.A, kMaxActions); return IRLMX_EINVAL; }
   if (!m.row_val) { set_error("row_val is NULL"); return IRLMX_EINVAL; }
   if (m.stencil) {
-    if ((long long)m.W * m.H != m.S) { set_error("stencil grid %dx%d != %d states", m.W, m.H, m.S); return IRLMX_EINVAL; }
+    if (m.W <= 0 || m.H <= 0 || (long long)m.W * m.H != m.S) {
+      set_error("stencil grid %dx%d != %d states", m.W, m.H, m.S);
+      return IRLMX_EINVAL;
+    }
   } else if (mdp->layout == IRLMX_LAYOUT_ELL) {
     if (!m.row_idx || m.K <= 0) { set_error("ELL row form missing"); return IRLMX_EINVAL; }
+    if (m.K > m.S) { set_error("ELL k_row=%d out of range (1..%d)", m.K, m.S); return IRLMX_EINVAL; }
   } else if (m.dense) {
     if (!m.col_val) { set_error("DENSE action-summed rows (col_val) missing"); return IRLMX_EINVAL; }
     if ((long long)m.S * m.S * m.A > (1LL << 40)) { set_error("DENSE table too large (S=%d)", m.S); return IRLMX_EINVAL; }
@@ -1466,6 +1482,21 @@ static int validate(const irlmx_mdp* mdp) {
     set_error("unknown layout %d", mdp->layout);
     return IRLMX_EINVAL;
   }
+  return 0;
+}
+
+// Required array arguments of an entry point: NULL is rejected before any work
+// is enqueued (a null device pointer would fault the GPU).
+struct Arg {
+  const void* p;
+  const char* name;  // nullptr: optional argument
+};
+static int need_all(const char* fn, std::initializer_list<Arg> args) {
+  for (const Arg& a : args)
+    if (a.name && !a.p) {
+      set_error("%s: %s is NULL", fn, a.name);
+      return IRLMX_EINVAL;
+    }
   return 0;
 }
 
@@ -1517,43 +1548,19 @@ static DenseBufs dense_bufs(const Ws& ws) {
 // M [S x S] . ZS [S x B].  Measured on MI355X (tools/diag/dense_bench.py,
 // profiles/r02_dense_gemm_bench.txt, microseconds per sweep):
 //
-//            streaming (VALU)      hand-written fp64 MFMA     rocBLAS dgemm
+//            streaming (VALU)      hand-written fp64 MFMA     rocBLAS dgemm (round 2, since dropped)
 //   S=2048   B=4 16  B=16 40  B=64 112   16 / 19 / 43           117 / 117 / 117
 //   S=4096   B=4 81  B=16 303 B=64 1227  29 / 34 / 80           447 / 448 / 450
 //
 // Streaming re-reads M from the 256 MB last-level cache, so it wins for few
-// instances while M is small; the MFMA kernel (dense.hip dense_gemm_kernel) wins
-// from 16 instances on, and from 4 on once M leaves that cache (S >= 4096).  The
-// library dgemm (fp64 MFMA kernels too, rocprof: Cijk_..._MI16x16x4x1) is the
-// fallback for S % 4 != 0 and is used only where it beats streaming.
-// IRLMX_DENSE_GEMM_MIN=<B> forces the batch threshold alone.
+// instances while M is small; the MFMA kernel (dense.hip dense_gemm_kernel, any
+// S: zero-padded K tail) wins from 16 instances on, and from 4 on once M leaves
+// that cache (S >= 4096).  IRLMX_DENSE_GEMM_MIN=<B> forces the batch threshold.
 static bool dense_gemm(const Model& m) {
   if (!m.dense || !m.shared) return false;
   const int forced = getenv_int("IRLMX_DENSE_GEMM_MIN", 0);
   if (forced > 0) return m.B >= forced;
-  if (dense_gemm_mfma_ok(m.S)) return m.B >= 16 || (m.S >= 4096 && m.B >= 4);
-  return m.S >= 4096 && m.B >= 32;
-}
-
-// one rocBLAS handle per host thread and device (handles are not thread safe)
-static int rocblas_for(hipStream_t st, rocblas_handle* out) {
-  struct Handles {
-    rocblas_handle h[64] = {};
-    ~Handles() {
-      for (auto& x : h)
-        if (x) rocblas_destroy_handle(x);
-    }
-  };
-  static thread_local Handles handles;
-  int dev = 0;
-  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) { set_error("rocblas: bad device"); return IRLMX_EHIP; }
-  if (!handles.h[dev] && rocblas_create_handle(&handles.h[dev]) != rocblas_status_success) {
-    set_error("rocblas_create_handle failed");
-    return IRLMX_EHIP;
-  }
-  if (rocblas_set_stream(handles.h[dev], st) != rocblas_status_success) { set_error("rocblas_set_stream failed"); return IRLMX_EHIP; }
-  *out = handles.h[dev];
-  return 0;
+  return m.B >= 16 || (m.S >= 4096 && m.B >= 4);
 }
 
 static int dense_backward(const Model& m, const double* reward, const uint8_t* terminal, int rescale,
@@ -1563,30 +1570,17 @@ static int dense_backward(const Model& m, const double* reward, const uint8_t* t
   dense_bwd_init_launch(d, terminal, w, st);
   const long long collapsed = 2LL * m.S - 1;
   const bool gemm = dense_gemm(m);
-  // GEMM engine: the hand-written fp64 MFMA kernel (dense.hip dense_gemm_kernel), or
-  // the library dgemm (IRLMX_DENSE_GEMM_ENGINE=rocblas; also for S % 4 != 0)
-  const char* eng = getenv("IRLMX_DENSE_GEMM_ENGINE");
-  const bool lib = (eng && strcmp(eng, "rocblas") == 0) || !dense_gemm_mfma_ok(m.S);
-  rocblas_handle h = nullptr;
-  if (gemm && lib)
-    if (int rc = rocblas_for(st, &h)) return rc;
-  const double one = 1.0, zero = 0.0;
   int r3 = 0;
   for (long long it = 0; it < collapsed; ++it) {
     if (gemm) {
-      // column-major view: C [S x B] = op(M) . ZS with M row-major = (M^T col-major), op = transpose
+      // C [B][S] = ZS . M^T on the hand-written fp64 MFMA kernel, then the per-state update
       const double* zin = (it & 1) ? ws.buf1 : ws.buf0;
-      if (!lib) {
-        dense_gemm_launch(m.col_val, zin, ws.wgt, m.S, m.S, m.B, st);
-      } else if (rocblas_dgemm(h, rocblas_operation_transpose, rocblas_operation_none, m.S, m.B, m.S, &one,
-                               m.col_val, m.S, zin, m.S, &zero, ws.wgt, m.S) != rocblas_status_success) {
-        set_error("rocblas_dgemm failed");
-        return IRLMX_EHIP;
-      }
+      if (hipError_t e = dense_gemm_launch(m.col_val, zin, ws.wgt, m.S, m.S, m.B, st)) return hip_fail(e, "dense gemm");
       dense_bwd_gemm_epilogue_launch(d, reward, rescale, w, it, r3, st);
     } else {
       dense_bwd_sweep_launch(d, reward, rescale, w, it, r3, st);
     }
+    if (hipError_t e = hipGetLastError()) return hip_fail(e, "dense backward sweep");
     r3 = r3 == 2 ? 0 : r3 + 1;
   }
   dense_bwd_final_launch(d, reward, rescale, p_action, status, w, collapsed, r3, st);
@@ -1601,7 +1595,9 @@ using namespace irlmx;
 extern "C" int irlmx_dense_to_rows(const double* dense, int32_t n_states, int32_t n_actions, double* p_rows,
                                    double* m_rows, void* stream) {
   if (!dense || !p_rows || !m_rows || n_states <= 0 || n_actions <= 0 || n_actions > kMaxActions) {
-    set_error("dense_to_rows: bad arguments");
+    set_error("dense_to_rows: bad arguments (n_states=%d, n_actions=%d in 1..%d, dense %s, p_rows %s, m_rows %s)",
+              n_states, n_actions, kMaxActions, dense ? "set" : "NULL", p_rows ? "set" : "NULL",
+              m_rows ? "set" : "NULL");
     return IRLMX_EINVAL;
   }
   dense_rows_launch(dense, n_states, n_actions, p_rows, m_rows, (hipStream_t)stream);
@@ -1617,7 +1613,11 @@ extern "C" size_t irlmx_workspace_bytes(const irlmx_mdp* mdp, int32_t op) {
 extern "C" int irlmx_execution_plan(const irlmx_mdp* mdp, int32_t op, int64_t* plan) {
   if (int rc = validate(mdp)) return rc;
   if (!plan) { set_error("plan is NULL"); return IRLMX_EINVAL; }
+  // (a backward call with rescale = 0 never takes the cluster shape: see irlmx_backward_maxent)
+  const bool no_rescale = op > 0 && (op & IRLMX_PLAN_NO_RESCALE) != 0;
+  if (no_rescale) op &= ~IRLMX_PLAN_NO_RESCALE;
   if (op < IRLMX_OP_BACKWARD || op > IRLMX_OP_VALUE_ITERATION) { set_error("unknown op %d", op); return IRLMX_EINVAL; }
+  if (no_rescale && op != IRLMX_OP_BACKWARD) { set_error("IRLMX_PLAN_NO_RESCALE applies to IRLMX_OP_BACKWARD only"); return IRLMX_EINVAL; }
   const Model m = make_model(mdp);
   for (int i = 0; i < IRLMX_PLAN_LEN; ++i) plan[i] = 0;
   FusedShape fs;
@@ -1631,7 +1631,8 @@ extern "C" int irlmx_execution_plan(const irlmx_mdp* mdp, int32_t op, int64_t* p
   }
   ClusterPlan cp;
   const int mode = op == IRLMX_OP_FORWARD ? kModeFwd : kModeBwd;
-  if (m.stencil && (op == IRLMX_OP_FORWARD || op == IRLMX_OP_BACKWARD) && cluster_plan(m.W, m.H, m.B, mode, &cp)) {
+  if (m.stencil && (op == IRLMX_OP_FORWARD || (op == IRLMX_OP_BACKWARD && !no_rescale && m.A <= kMaxActions)) &&
+      cluster_plan(m.W, m.H, m.B, mode, &cp)) {
     plan[0] = IRLMX_SHAPE_CLUSTER;
     plan[1] = cp.R; plan[2] = cp.G; plan[3] = cp.C; plan[4] = cp.per_launch; plan[5] = cp.spt;
     plan[6] = cp.pair; plan[7] = cp.nt; plan[8] = (m.B + cp.per_launch - 1) / cp.per_launch;
@@ -1650,8 +1651,7 @@ extern "C" int irlmx_execution_plan(const irlmx_mdp* mdp, int32_t op, int64_t* p
     return 0;
   }
   if (m.dense) {
-    const bool gemm = op == IRLMX_OP_BACKWARD ? dense_gemm(m)
-                      : (op != IRLMX_OP_FORWARD && dense_gemm(m) && dense_gemm_mfma_ok(m.S));
+    const bool gemm = op != IRLMX_OP_FORWARD && dense_gemm(m);
     plan[0] = gemm ? IRLMX_SHAPE_DENSE_GEMM : IRLMX_SHAPE_DENSE;
     plan[7] = kDenseThreads;
     plan[9] = dense_lds_vec(dense_view(m)) ? (int64_t)m.S * 8 : 0;
@@ -1669,6 +1669,10 @@ extern "C" int irlmx_forward_svf(const irlmx_mdp* mdp, const double* p_initial, 
   if (int rc = validate(mdp)) return rc;
   const Model m = make_model(mdp);
   if (!m.stencil && !m.dense && (!m.col_idx || !m.col_val || m.Kc <= 0)) { set_error("ELL column form missing"); return IRLMX_EINVAL; }
+  if (!m.stencil && !m.dense && m.Kc > m.S) { set_error("ELL k_col=%d out of range (1..%d)", m.Kc, m.S); return IRLMX_EINVAL; }
+  if (int rc = need_all("forward_svf", {{p_initial, "p_initial"}, {terminal, "terminal"}, {p_action, "p_action"},
+                                        {svf, "svf"}, {iterations, "iterations"}, {status, "status"}}))
+    return rc;
   if (int rc = check_ws(m, IRLMX_OP_FORWARD, workspace_bytes, workspace)) return rc;
   hipStream_t st = (hipStream_t)stream;
   Ws ws = carve(m, IRLMX_OP_FORWARD, workspace);
@@ -1710,6 +1714,7 @@ extern "C" int irlmx_forward_svf(const irlmx_mdp* mdp, const double* p_initial, 
     // bookkeeping is exact (same arithmetic, bit-identical results); likewise
     // when the tiles could not all run at once (another kernel holds CUs)
     persistent = rc != kClusterNotResident;
+    if (rc == kClusterNonFinite) count_event(IRLMX_CTR_RERUN_NONFINITE);
     e = hipMemsetAsync(workspace, 0, ws.total, st);
     if (e != hipSuccess) return hip_fail(e, "workspace memset");
     hipLaunchKernelGGL(fwd_weights_kernel, g, dim3(256), 0, st, m, p_action, terminal, ws.wgt, ws.bad);
@@ -1723,6 +1728,7 @@ extern "C" int irlmx_forward_svf(const irlmx_mdp* mdp, const double* p_initial, 
     if (rc != kClusterNotResident) return rc;  // else: the per-sweep shape below
   }
   const dim3 gs((m.S + kSweepThreads - 1) / kSweepThreads, m.B);
+  count_event(IRLMX_CTR_SWEEP_CALLS);
   int rc = run_until_done(ws, m.B, st, [&](long long it, int r3) {
     hipLaunchKernelGGL(fwd_sweep_kernel, gs, dim3(kSweepThreads), 0, st, a, ws, it, r3);
   });
@@ -1737,6 +1743,9 @@ extern "C" int irlmx_backward_maxent(const irlmx_mdp* mdp, const double* reward,
                                      size_t workspace_bytes, void* stream) {
   if (int rc = validate(mdp)) return rc;
   const Model m = make_model(mdp);
+  if (int rc = need_all("backward_maxent",
+                        {{reward, "reward"}, {terminal, "terminal"}, {p_action, "p_action"}, {status, "status"}}))
+    return rc;
   if (int rc = check_ws(m, IRLMX_OP_BACKWARD, workspace_bytes, workspace)) return rc;
   hipStream_t st = (hipStream_t)stream;
   Ws ws = carve(m, IRLMX_OP_BACKWARD, workspace);
@@ -1788,6 +1797,7 @@ extern "C" int irlmx_backward_maxent(const irlmx_mdp* mdp, const double* reward,
     if (rc != kClusterNotResident) return rc;  // else: the per-sweep shape below
   }
   const dim3 g((m.S + kSweepThreads - 1) / kSweepThreads, m.B);
+  count_event(IRLMX_CTR_SWEEP_CALLS);
   hipLaunchKernelGGL(bwd_init_kernel, g, dim3(kSweepThreads), 0, st, a, ws);
   const long long collapsed = 2LL * m.S - 1;
   int r3 = 0;
@@ -1807,6 +1817,11 @@ static int bellman_common(const irlmx_mdp* mdp, const double* reward, const doub
   if (int rc = validate(mdp)) return rc;
   const Model m = make_model(mdp);
   const int op = soft ? IRLMX_OP_SOFT_BACKWARD : IRLMX_OP_VALUE_ITERATION;
+  if (int rc = need_all(soft ? "soft_backward" : "value_iteration",
+                        {{reward, "reward"}, {phi, soft ? "terminal_reward" : nullptr},
+                         {p_action, soft ? "p_action" : nullptr}, {value, soft ? nullptr : "value"},
+                         {iterations, "iterations"}, {status, "status"}}))
+    return rc;
   if (int rc = check_ws(m, op, workspace_bytes, workspace)) return rc;
   hipStream_t st = (hipStream_t)stream;
   Ws ws = carve(m, op, workspace);
@@ -1831,11 +1846,17 @@ static int bellman_common(const irlmx_mdp* mdp, const double* reward, const doub
     const DenseBufs w = dense_bufs(ws);
     const DenseBellman db{reward, phi, discount, eps, (long long)max_iter, average, soft ? 1 : 0, p_action, value,
                           iterations, status};
-    const bool gemm = dense_gemm(m) && dense_gemm_mfma_ok(m.S);  // the P . [v_1 .. v_B] products on the MFMA kernel
+    const bool gemm = dense_gemm(m);  // the P . [v_1 .. v_B] products on the MFMA kernel
+    hipError_t gerr = hipSuccess;
     int rc = run_until_done(ws, m.B, st, [&](long long it, int r3) {
-      if (gemm) dense_bellman_gemm_sweep_launch(d, db, w, it, r3, st);
-      else dense_bellman_sweep_launch(d, db, w, it, r3, st);
+      if (gemm) {
+        const hipError_t e = dense_bellman_gemm_sweep_launch(d, db, w, it, r3, st);
+        if (e != hipSuccess && gerr == hipSuccess) gerr = e;
+      } else {
+        dense_bellman_sweep_launch(d, db, w, it, r3, st);
+      }
     });
+    if (gerr != hipSuccess) return hip_fail(gerr, "dense gemm");
     if (rc) return rc;
     dense_bellman_finish_launch(d, db, w, st);
     e = hipGetLastError();
@@ -1848,6 +1869,7 @@ static int bellman_common(const irlmx_mdp* mdp, const double* reward, const doub
     const int rc = grid_launch(m, op, gp, args, ws, st);
     if (rc != kClusterNotResident) return rc;  // else: the per-sweep shape below
   }
+  count_event(IRLMX_CTR_SWEEP_CALLS);
   int rc = run_until_done(ws, m.B, st, [&](long long it, int r3) {
     if (soft) hipLaunchKernelGGL(bellman_sweep_kernel<true>, gb, dim3(bt), 0, st, a, ws, it, r3);
     else hipLaunchKernelGGL(bellman_sweep_kernel<false>, gb, dim3(bt), 0, st, a, ws, it, r3);
@@ -1872,4 +1894,26 @@ extern "C" int irlmx_value_iteration(const irlmx_mdp* mdp, const double* reward,
                                      int32_t* status, void* workspace, size_t workspace_bytes, void* stream) {
   return bellman_common(mdp, reward, nullptr, discount, eps, max_iter, average, nullptr, value, iterations,
                         status, workspace, workspace_bytes, stream, false);
+}
+
+extern "C" int irlmx_dense_gemm(const double* m, const double* z, double* c, int32_t rows, int32_t n, int32_t batch,
+                                void* stream) {
+  if (!m || !z || !c || rows <= 0 || n <= 0 || batch <= 0) {
+    set_error("dense_gemm: bad arguments (rows=%d, n=%d, batch=%d, m %s, z %s, c %s)", rows, n, batch,
+              m ? "set" : "NULL", z ? "set" : "NULL", c ? "set" : "NULL");
+    return IRLMX_EINVAL;
+  }
+  const hipError_t e = dense_gemm_launch(m, z, c, rows, n, batch, (hipStream_t)stream);
+  return e == hipSuccess ? 0 : hip_fail(e, "dense_gemm");
+}
+
+extern "C" int irlmx_dense_gemm_variant(int32_t rows, int32_t n, int32_t batch, int32_t* variant) {
+  if (!variant || rows <= 0 || n <= 0 || batch <= 0) {
+    set_error("dense_gemm_variant: bad arguments");
+    return IRLMX_EINVAL;
+  }
+  int v[4];
+  dense_gemm_variant(rows, n, batch, v);
+  for (int i = 0; i < 4; ++i) variant[i] = v[i];
+  return 0;
 }

@@ -16,6 +16,9 @@
 
 namespace irlmx {
 
+// largest grid side / state count the 32-bit state indices of the kernels cover
+constexpr int kMaxSide = 46340;                    // size * size < 2^31
+constexpr long long kMaxStates = 46340LL * 46340LL;
 void set_error(const char* fmt, ...);
 int hip_fail(hipError_t e, const char* what);
 
@@ -140,7 +143,11 @@ using namespace irlmx;
 
 extern "C" int irlmx_build_icy_gridworld(int32_t size, const double* p_slip, int32_t batch, double* row_val,
                                          void* stream) {
-  if (size <= 0 || batch <= 0 || !p_slip || !row_val) { set_error("build_icy_gridworld: bad arguments"); return IRLMX_EINVAL; }
+  if (size <= 0 || size > kMaxSide || batch <= 0 || !p_slip || !row_val) {
+    set_error("build_icy_gridworld: bad arguments (size=%d, batch=%d, p_slip %s, row_val %s)", size, batch,
+              p_slip ? "set" : "NULL", row_val ? "set" : "NULL");
+    return IRLMX_EINVAL;
+  }
   const int S = size * size;
   hipLaunchKernelGGL(icy_gridworld_kernel, dim3((S + 255) / 256, batch), dim3(256), 0, (hipStream_t)stream, size,
                      p_slip, row_val);
@@ -149,7 +156,10 @@ extern "C" int irlmx_build_icy_gridworld(int32_t size, const double* p_slip, int
 }
 
 extern "C" int irlmx_build_gridworld(int32_t size, int32_t batch, double* row_val, void* stream) {
-  if (size <= 0 || batch <= 0 || !row_val) { set_error("build_gridworld: bad arguments"); return IRLMX_EINVAL; }
+  if (size <= 0 || size > kMaxSide || batch <= 0 || !row_val) {
+    set_error("build_gridworld: bad arguments (size=%d, batch=%d, row_val %s)", size, batch, row_val ? "set" : "NULL");
+    return IRLMX_EINVAL;
+  }
   const int S = size * size;
   hipLaunchKernelGGL(gridworld_kernel, dim3((S + 255) / 256, batch), dim3(256), 0, (hipStream_t)stream, size, row_val);
   hipError_t e = hipGetLastError();
@@ -158,8 +168,11 @@ extern "C" int irlmx_build_gridworld(int32_t size, int32_t batch, double* row_va
 
 extern "C" int irlmx_dense_to_stencil(const double* dense, int32_t width, int32_t height, int32_t n_actions,
                                       double* row_val, int32_t* off_stencil, void* stream) {
-  if (width <= 0 || height <= 0 || n_actions <= 0 || !dense || !row_val || !off_stencil) {
-    set_error("dense_to_stencil: bad arguments");
+  if (width <= 0 || height <= 0 || (long long)width * height > kMaxStates || n_actions <= 0 || !dense || !row_val ||
+      !off_stencil) {
+    set_error("dense_to_stencil: bad arguments (width=%d, height=%d, n_actions=%d, dense %s, row_val %s, "
+              "off_stencil %s)", width, height, n_actions, dense ? "set" : "NULL", row_val ? "set" : "NULL",
+              off_stencil ? "set" : "NULL");
     return IRLMX_EINVAL;
   }
   hipStream_t st = (hipStream_t)stream;
@@ -178,7 +191,9 @@ extern "C" int irlmx_dense_to_stencil(const double* dense, int32_t width, int32_
 extern "C" int irlmx_optimal_policy(const int32_t* successor, int32_t n_states, int32_t n_actions, int32_t batch,
                                     const double* value, int64_t* policy, void* stream) {
   if (n_states <= 0 || n_actions <= 0 || batch <= 0 || !successor || !value || !policy) {
-    set_error("optimal_policy: bad arguments");
+    set_error("optimal_policy: bad arguments (n_states=%d, n_actions=%d, batch=%d, successor %s, value %s, "
+              "policy %s)", n_states, n_actions, batch, successor ? "set" : "NULL", value ? "set" : "NULL",
+              policy ? "set" : "NULL");
     return IRLMX_EINVAL;
   }
   hipLaunchKernelGGL(optimal_policy_kernel, dim3((n_states + 255) / 256, batch), dim3(256), 0, (hipStream_t)stream,
@@ -190,7 +205,9 @@ extern "C" int irlmx_optimal_policy(const int32_t* successor, int32_t n_states, 
 extern "C" int irlmx_stochastic_policy(const int32_t* successor, int32_t n_states, int32_t n_actions, int32_t batch,
                                        const double* weighted_value, double* p_policy, void* stream) {
   if (n_states <= 0 || n_actions <= 0 || batch <= 0 || !successor || !weighted_value || !p_policy) {
-    set_error("stochastic_policy: bad arguments");
+    set_error("stochastic_policy: bad arguments (n_states=%d, n_actions=%d, batch=%d, successor %s, "
+              "weighted_value %s, p_policy %s)", n_states, n_actions, batch, successor ? "set" : "NULL",
+              weighted_value ? "set" : "NULL", p_policy ? "set" : "NULL");
     return IRLMX_EINVAL;
   }
   hipLaunchKernelGGL(stochastic_policy_kernel, dim3((n_states + 255) / 256, batch), dim3(256), 0,
@@ -289,8 +306,9 @@ __global__ void ell_cols_kernel(const double* __restrict__ dense, int S, int A, 
 
 extern "C" int irlmx_dense_ell_sizes(const double* dense, int32_t n_states, int32_t n_actions, int32_t* k_out,
                                      int32_t* col_count, void* stream) {
-  if (n_states <= 0 || n_actions <= 0 || !dense || !k_out || !col_count) {
-    set_error("dense_ell_sizes: bad arguments");
+  if (n_states <= 0 || n_states > kMaxStates || n_actions <= 0 || !dense || !k_out || !col_count) {
+    set_error("dense_ell_sizes: bad arguments (n_states=%d, n_actions=%d, dense %s, k_out %s, col_count %s)",
+              n_states, n_actions, dense ? "set" : "NULL", k_out ? "set" : "NULL", col_count ? "set" : "NULL");
     return IRLMX_EINVAL;
   }
   hipStream_t st = (hipStream_t)stream;
@@ -309,9 +327,10 @@ extern "C" int irlmx_dense_ell_sizes(const double* dense, int32_t n_states, int3
 extern "C" int irlmx_dense_to_ell(const double* dense, int32_t n_states, int32_t n_actions, int32_t k_row,
                                   int32_t k_col, int32_t* row_idx, double* row_val, int32_t* col_idx,
                                   double* col_val, void* stream) {
-  if (n_states <= 0 || n_actions <= 0 || k_row <= 0 || k_col <= 0 || !dense || !row_idx || !row_val ||
-      !col_idx || !col_val) {
-    set_error("dense_to_ell: bad arguments");
+  if (n_states <= 0 || n_states > kMaxStates || n_actions <= 0 || k_row <= 0 || k_col <= 0 || k_row > n_states ||
+      k_col > n_states || !dense || !row_idx || !row_val || !col_idx || !col_val) {
+    set_error("dense_to_ell: bad arguments (n_states=%d, n_actions=%d, k_row=%d, k_col=%d; k in 1..n_states, "
+              "every array non-NULL)", n_states, n_actions, k_row, k_col);
     return IRLMX_EINVAL;
   }
   hipStream_t st = (hipStream_t)stream;

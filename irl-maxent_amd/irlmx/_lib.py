@@ -24,6 +24,10 @@ LAYOUT_DENSE = 3
 SUCCESS = 0
 OK, NONFINITE, MAXITER = 0, 1, 2
 OP_BACKWARD, OP_FORWARD, OP_SOFT_BACKWARD, OP_VALUE_ITERATION = 1, 2, 3, 4
+PLAN_NO_RESCALE = 0x100
+EINVAL, EHIP, EWORKSPACE = -1, -2, -3
+COUNTER_NAMES = ("cluster_launches", "grid_launches", "rerun_nonfinite", "rerun_not_resident", "rerun_timeout",
+                 "sweep_calls")   # IRLMX_CTR_* order
 
 
 class IrlmxError(RuntimeError):
@@ -62,6 +66,7 @@ _MDP = ctypes.POINTER(MDPStruct)
 SIGNATURES = {
     "irlmx_abi_version": (ctypes.c_int, []),
     "irlmx_last_error": (ctypes.c_char_p, []),
+    "irlmx_counters": (ctypes.c_int, [_P, _I32]),
     "irlmx_workspace_bytes": (_SZ, [_MDP, _I32]),
     "irlmx_backward_maxent": (ctypes.c_int, [_MDP, _P, _P, _I32, _P, _P, _P, _SZ, _P]),
     "irlmx_forward_svf": (ctypes.c_int, [_MDP, _P, _P, _P, _D, _I64, _P, _P, _P, _P, _SZ, _P]),
@@ -76,6 +81,8 @@ SIGNATURES = {
     "irlmx_dense_to_rows": (ctypes.c_int, [_P, _I32, _I32, _P, _P, _P]),
     "irlmx_dense_ell_sizes": (ctypes.c_int, [_P, _I32, _I32, _P, _P, _P]),
     "irlmx_dense_to_ell": (ctypes.c_int, [_P, _I32, _I32, _I32, _I32, _P, _P, _P, _P, _P]),
+    "irlmx_dense_gemm": (ctypes.c_int, [_P, _P, _P, _I32, _I32, _I32, _P]),
+    "irlmx_dense_gemm_variant": (ctypes.c_int, [_I32, _I32, _I32, _P]),
 }
 
 _lib = None

@@ -18,6 +18,19 @@ repeats steps until every instance has met the reference's stopping rule
 does); a stopped instance's theta is frozen, so each instance ends exactly
 where its own reference loop would.
 
+Compaction (``run(compact=True)``, the default): once an instance has
+stopped, the following steps run only the still-active instances -- their
+tables, demonstration statistics and theta are gathered into a smaller batch
+(``DeviceMDP.take``) and the kernels re-plan for it (fewer instances: more
+CUs per instance) -- so a stopped instance no longer pays its 2*S backward
+sweeps and its forward pass every step.  Per-instance results do not depend on
+the batch they run in (every kernel shape and plan performs the same float64
+operations in the same order per instance), so a compacted run equals an
+uncompacted one bit for bit with identity features
+(tests/test_gpu_full_run.py); with a feature matrix the F . theta / F^T . svf
+products are torch GEMMs whose summation order may change with the batch size
+(rounding-level differences).
+
 No host round trip happens inside a step except the forward pass's own
 convergence polling on the per-sweep shape.
 """
@@ -62,6 +75,7 @@ class BatchedMaxEnt:
         self.p_initial = torch.as_tensor(p_initial, dtype=torch.float64, device=dev).reshape(B, S)
         self.terminal = ops.terminal_mask(terminal, S, batch=B, device=dev)
         self.causal = causal
+        self.phi = None
         if causal:
             if discount is None:
                 raise ValueError("causal IRL needs a discount (maxent.py:383)")
@@ -75,47 +89,114 @@ class BatchedMaxEnt:
         self.k = 0
         self.active = torch.ones(B, dtype=torch.bool, device=dev)
         self.steps = torch.zeros(B, dtype=torch.int64, device=dev)
-        self.last_forward_sweeps = None
+        self.last_forward_sweeps = None    # [B] int64, 0 for instances not computed in the last step
         self.last_backward_sweeps = None   # causal: soft VI sweeps of the last backward() [B]
         self.last_delta = None
+        self._work = None                  # compacted working set (compact()), None = all instances
+
+    @property
+    def batch(self):
+        return self.mdp.batch
+
+    @property
+    def working_batch(self):
+        """Instances the next step computes (all, or the active ones after compact())."""
+        return self.batch if self._work is None else int(self._work["idx"].numel())
 
     def lr(self, k):
         return self.lr0 / (1.0 + float(k))   # linear_decay(lr0, 1, 1)
 
-    def reward(self):
-        """F . theta, [B, S] (maxent.py:244)."""
-        if self.features is None:
-            return self.theta
-        if self.features.dim() == 2:
-            return self.theta @ self.features.T
-        return torch.bmm(self.features, self.theta.unsqueeze(2)).squeeze(2)
+    # -- working set ----------------------------------------------------------
 
-    def features_t(self, svf):
-        """F^T . svf, [B, F] (maxent.py:248)."""
-        if self.features is None:
+    def compact(self):
+        """Restrict the following steps to the instances that are still active.
+
+        Gathers their tables, demonstration statistics, masks and features into a
+        smaller batch; theta stays full size (the working rows are gathered and
+        scattered per step).  Returns the working batch size."""
+        idx = torch.nonzero(self.active).squeeze(1)
+        n = int(idx.numel())
+        if n == self.working_batch:
+            return n
+        sel = lambda t: t.index_select(0, idx).contiguous() if t is not None else None
+        feats = self.features
+        if feats is not None and feats.dim() == 3:
+            feats = sel(feats)
+        self._work = {"idx": idx, "mdp": self.mdp.take(idx), "e_features": sel(self.e_features),
+                      "p_initial": sel(self.p_initial), "terminal": sel(self.terminal), "phi": sel(self.phi),
+                      "features": feats, "active": torch.ones(n, dtype=torch.bool, device=idx.device)}
+        return n
+
+    def _w(self, name):
+        if self._work is None:
+            return getattr(self, name)
+        return self._work[name]
+
+    def _theta_w(self):
+        return self.theta if self._work is None else self.theta.index_select(0, self._work["idx"])
+
+    def _active_w(self):
+        return self.active if self._work is None else self.active.index_select(0, self._work["idx"])
+
+    def _scatter(self, vec_w, fill=0):
+        """A per-instance vector of the working set, expanded to all B instances."""
+        if self._work is None:
+            return vec_w
+        out = torch.full((self.batch,) + tuple(vec_w.shape[1:]), fill, dtype=vec_w.dtype, device=vec_w.device)
+        out[self._work["idx"]] = vec_w
+        return out
+
+    # -- one gradient step --------------------------------------------------
+
+    def reward(self, theta=None, features=None):
+        """F . theta (maxent.py:244): [B, S] for all instances by default."""
+        if theta is None:
+            theta, features = self.theta, self.features
+        if features is None:
+            return theta
+        if features.dim() == 2:
+            return theta @ features.T
+        return torch.bmm(features, theta.unsqueeze(2)).squeeze(2)
+
+    def features_t(self, svf, features=None):
+        """F^T . svf, [n, F] (maxent.py:248)."""
+        if features is None:
+            features = self._w("features")
+        if features is None:
             return svf
-        if self.features.dim() == 2:
-            return svf @ self.features
-        return torch.bmm(svf.unsqueeze(1), self.features).squeeze(1)
+        if features.dim() == 2:
+            return svf @ features
+        return torch.bmm(svf.unsqueeze(1), features).squeeze(1)
 
     def backward(self):
-        r = self.reward()
+        """Policy [n, S, A] of the working set (maxent.py:119-159 / 279-341)."""
+        r = self.reward(self._theta_w(), self._w("features"))
+        mdp = self._w("mdp")
         if self.causal:
-            pi, _, k, _ = ops.soft_backward(self.mdp, r, self.phi, self.discount, self.eps_lap)
-            self.last_backward_sweeps = k
+            pi, _, k, _ = ops.soft_backward(mdp, r, self._w("phi"), self.discount, self.eps_lap)
+            self.last_backward_sweeps = self._scatter(k)
             return pi
-        return ops.backward_maxent(self.mdp, r, self.terminal, rescale=self.rescale)
+        return ops.backward_maxent(mdp, r, self._w("terminal"), rescale=self.rescale)
 
     def forward(self, pi):
-        return ops.forward_svf(self.mdp, self.p_initial, self.terminal, pi, self.eps_esvf)
+        """``(svf [n, S], sweeps [n], status [n])`` of the working set (maxent.py:63-114)."""
+        return ops.forward_svf(self._w("mdp"), self._w("p_initial"), self._w("terminal"), pi, self.eps_esvf)
 
     def update(self, svf):
-        grad = self.e_features - self.features_t(svf)
-        new = self.theta * torch.exp(self.lr(self.k) * grad)
-        act = self.active.unsqueeze(1)
-        self.last_delta = torch.where(self.active, (new - self.theta).abs().amax(dim=1),
-                                      torch.zeros((), dtype=torch.float64, device=self.theta.device))
-        self.theta = torch.where(act, new, self.theta)   # stopped instances stay frozen
+        """ExpSga step on the working set's theta (optimizer.py:154-167); stopped
+        instances stay frozen.  Returns the gradient [n, F]."""
+        theta = self._theta_w()
+        act = self._active_w()
+        grad = self._w("e_features") - self.features_t(svf)
+        new = theta * torch.exp(self.lr(self.k) * grad)
+        delta = torch.where(act, (new - theta).abs().amax(dim=1),
+                            torch.zeros((), dtype=torch.float64, device=theta.device))
+        new = torch.where(act.unsqueeze(1), new, theta)
+        if self._work is None:
+            self.theta = new
+        else:
+            self.theta[self._work["idx"]] = new
+        self.last_delta = self._scatter(delta)
         self.steps += self.active.to(torch.int64)
         self.k += 1
         return grad
@@ -123,19 +204,25 @@ class BatchedMaxEnt:
     def step(self):
         pi = self.backward()
         svf, iters, _ = self.forward(pi)
-        self.last_forward_sweeps = iters
+        self.last_forward_sweeps = self._scatter(iters)
         self.update(svf)
         return svf
 
-    def run(self, eps=1e-4, max_steps=None):
+    def run(self, eps=1e-4, max_steps=None, compact=True, on_step=None):
         """Step until every instance meets ``max|dtheta| <= eps`` (maxent.py:240, 252).
 
+        ``compact``: drop stopped instances from the working set before each
+        step (module docstring).  ``on_step(self)`` is called after every step.
         Returns ``(reward [B, S], steps [B])`` -- ``features . theta`` and the
         number of gradient steps each instance took.
         """
         while bool(self.active.any()):
             if max_steps is not None and self.k >= max_steps:
                 break
+            if compact:
+                self.compact()
             self.step()
             self.active &= self.last_delta > eps   # NaN > eps is False: a NaN step stops
+            if on_step is not None:
+                on_step(self)
         return self.reward(), self.steps

@@ -40,11 +40,25 @@ def stencil_targets(size):
                      np.where(y + 1 < size, s + size, -1), np.where(y > 0, s - size, -1)], axis=1)
 
 
-def sample(row_val, size, terminal, start, n=200, seed=0, beta=2.0, max_len=None):
+class TruncatedDemonstrations(ValueError):
+    """Some trajectories were cut at ``max_len`` before reaching a terminal state."""
+
+
+def sample(row_val, size, terminal, start, n=200, seed=0, beta=2.0, max_len=None, on_truncate="raise",
+           with_truncated=False):
     """Sample ``n`` demonstrations on one STENCIL5 table ``row_val`` [4, 5, S].
 
-    Returns ``(e_features, p_initial, lengths)`` for identity state features.
+    Like the reference (trajectory.py:76, ``while not terminal``) a trajectory
+    runs until it reaches a terminal state: with ``max_len=None`` there is no
+    cap.  With a cap, trajectories still alive after ``max_len`` steps are cut
+    (their last state then counts as a final state, which skews the feature
+    expectation): ``on_truncate="raise"`` raises TruncatedDemonstrations,
+    ``"allow"`` keeps them.  Returns ``(e_features, p_initial, lengths)`` for
+    identity state features, plus the number of cut trajectories when
+    ``with_truncated``.
     """
+    if on_truncate not in ("raise", "allow"):
+        raise ValueError(f"on_truncate must be 'raise' or 'allow', got {on_truncate!r}")
     rng = np.random.default_rng(seed)
     S = size * size
     goal = terminal[0]
@@ -58,9 +72,9 @@ def sample(row_val, size, terminal, start, n=200, seed=0, beta=2.0, max_len=None
     p_init = np.bincount(state, minlength=S) / n
     alive = ~is_term[state]
     lengths = np.zeros(n, dtype=np.int64)
-    max_len = max_len or 64 * size
-    for _ in range(max_len):
-        if not alive.any():
+    steps = 0
+    while alive.any():
+        if max_len is not None and steps >= max_len:
             break
         idx = np.nonzero(alive)[0]
         s = state[idx]
@@ -73,5 +87,11 @@ def sample(row_val, size, terminal, start, n=200, seed=0, beta=2.0, max_len=None
         state[idx] = nxt
         lengths[idx] += 1
         alive[idx] = ~is_term[nxt]
+        steps += 1
+    truncated = int(np.count_nonzero(alive))
+    if truncated and on_truncate == "raise":
+        raise TruncatedDemonstrations(f"{truncated} of {n} demonstrations did not reach a terminal state within "
+                                      f"max_len={max_len} steps (the reference samples until terminal)")
     np.add.at(counts, state, 1.0)                                  # final states (trajectory.py:43)
-    return counts / n, p_init, lengths
+    out = (counts / n, p_init, lengths)
+    return out + (truncated,) if with_truncated else out

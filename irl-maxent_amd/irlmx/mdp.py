@@ -89,12 +89,12 @@ class DeviceMDP:
         equal bit for bit to uploading the dense [S, S, 5] table, tested)."""
         if self.layout != _lib.LAYOUT_STENCIL5:
             raise ValueError("with_stay: STENCIL5 tables only")
-        B, A, K, S = self.row_val.shape
-        stay = torch.zeros((B, 1, K, S), dtype=self.row_val.dtype, device=self.row_val.device)
+        n_tab, A, K, S = self.row_val.shape   # tables held (1 for a shared model), not the instance count
+        stay = torch.zeros((n_tab, 1, K, S), dtype=self.row_val.dtype, device=self.row_val.device)
         stay[:, 0, 0, :] = 1.0                                     # slot 0 = the state itself
         row_val = torch.cat([self.row_val, stay], dim=1).contiguous()
-        return DeviceMDP(self.layout, S, A + 1, B, self.shared, row_val, width=self.width, height=self.height,
-                         device=self.device)
+        return DeviceMDP(self.layout, S, A + 1, self.batch, self.shared, row_val, width=self.width,
+                         height=self.height, device=self.device)
 
     #: ELL slots per state above which (and above S / 8) a table is kept DENSE
     DENSE_MIN_SLOTS = 32
@@ -211,6 +211,19 @@ class DeviceMDP:
         return DeviceMDP(self.layout, self.n_states, self.n_actions, hi - lo, False, sl(self.row_val),
                          sl(self.row_idx), sl(self.col_idx), sl(self.col_val), self.width, self.height,
                          self.k_row, self.k_col, self.device)
+
+    def take(self, index):
+        """Instances ``index`` (int64 device or host indices, in that order) as a
+        new model: a shared table is reused as is; per-instance tables are
+        gathered into fresh contiguous tensors (irlmx.batch compaction)."""
+        index = torch.as_tensor(index, dtype=torch.int64, device=self.device)
+        n = int(index.numel())
+        if self.shared:
+            return self.with_batch(n)
+        g = lambda t: t.index_select(0, index).contiguous() if t is not None else None
+        return DeviceMDP(self.layout, self.n_states, self.n_actions, n, False, g(self.row_val), g(self.row_idx),
+                         g(self.col_idx), g(self.col_val), self.width, self.height, self.k_row, self.k_col,
+                         self.device)
 
     def struct(self):
         """The ``irlmx_mdp`` C struct (pointers stay valid while self is alive)."""

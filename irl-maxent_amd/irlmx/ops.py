@@ -31,18 +31,31 @@ _OPS = {"backward": _lib.OP_BACKWARD, "forward": _lib.OP_FORWARD, "soft_backward
         "value_iteration": _lib.OP_VALUE_ITERATION}
 
 
-def execution_plan(mdp, op):
+def execution_plan(mdp, op, rescale=True):
     """The kernel plan a call of ``op`` ("backward", "forward", "soft_backward",
     "value_iteration") on ``mdp`` runs on the current device (irlmx_execution_plan):
     shape, tile rows R, ghost rows G, tiles per instance C, instances per launch,
-    states per lane, in-tile layout, threads, sequential launches, LDS bytes."""
+    states per lane, in-tile layout, threads, sequential launches, LDS bytes.
+    ``rescale=False``: the plan of ``backward_maxent(..., rescale=False)``."""
     import ctypes
     lib = _lib.load()
     buf = (ctypes.c_int64 * len(PLAN_FIELDS))()
-    _lib.check(lib.irlmx_execution_plan(mdp.struct(), _OPS[op], buf), "execution_plan")
+    code = _OPS[op] | (0 if rescale or op != "backward" else _lib.PLAN_NO_RESCALE)
+    _lib.check(lib.irlmx_execution_plan(mdp.struct(), code, buf), "execution_plan")
     plan = dict(zip(PLAN_FIELDS, [int(v) for v in buf]))
     plan["shape"] = SHAPES[plan["shape"]]
     return plan
+
+
+def counters():
+    """Process-wide event counters of the library (irlmx_counters): persistent
+    launches and per-sweep reruns, by name (``_lib.COUNTER_NAMES``)."""
+    import ctypes
+    lib = _lib.load()
+    buf = (ctypes.c_int64 * len(_lib.COUNTER_NAMES))()
+    n = lib.irlmx_counters(buf, len(_lib.COUNTER_NAMES))
+    assert n == len(_lib.COUNTER_NAMES), n
+    return dict(zip(_lib.COUNTER_NAMES, [int(v) for v in buf]))
 
 
 def _f64(x, mdp, shape):
@@ -137,6 +150,32 @@ def value_iteration(mdp, reward, discount, eps=1e-3, average=False, max_iter=0):
     return v, iters, status
 
 
+def dense_gemm(m, z):
+    """``z @ m.T`` on the fp64 matrix cores (irlmx_dense_gemm): m [R, S], z [B, S]
+    float64 device tensors -> [B, R].  The batched P . [v_1 .. v_B] contraction
+    of the DENSE layout's shared-table sweeps."""
+    lib = _lib.load()
+    m = m.to(dtype=torch.float64).contiguous()
+    z = z.to(dtype=torch.float64, device=m.device).contiguous()
+    (R, S), (B, S2) = m.shape, z.shape
+    if S2 != S:
+        raise ValueError(f"dense_gemm: m is {tuple(m.shape)}, z is {tuple(z.shape)}")
+    c = torch.empty((B, R), dtype=torch.float64, device=m.device)
+    _lib.check(lib.irlmx_dense_gemm(_lib.ptr(m), _lib.ptr(z), _lib.ptr(c), R, S, B, _lib.stream_ptr(m.device)),
+               "dense_gemm")
+    return c
+
+
+def dense_gemm_variant(rows, n, batch):
+    """(row tiles, instance tiles, waves, 16-byte loads) of the MFMA kernel a
+    dense_gemm of these sizes launches."""
+    import ctypes
+    lib = _lib.load()
+    v = (ctypes.c_int32 * 4)()
+    _lib.check(lib.irlmx_dense_gemm_variant(rows, n, batch, v), "dense_gemm_variant")
+    return tuple(int(x) for x in v)
+
+
 def optimal_policy(successor, value):
     """argmax_a value[successor[s, a]] per state, first index on ties (solver.py:107-124)."""
     lib = _lib.load()
@@ -163,5 +202,5 @@ def stochastic_policy(successor, weighted_value):
     return out
 
 
-__all__ = ["DeviceMDP", "execution_plan", "terminal_mask", "backward_maxent", "forward_svf", "soft_backward",
-           "value_iteration", "optimal_policy", "stochastic_policy"]
+__all__ = ["DeviceMDP", "execution_plan", "counters", "terminal_mask", "backward_maxent", "forward_svf", "soft_backward",
+           "value_iteration", "dense_gemm", "dense_gemm_variant", "optimal_policy", "stochastic_policy"]

@@ -2,8 +2,9 @@
 
 Transition models whose rows are mostly nonzero (non-grid MDPs) are kept as
 per-action S x S row-major matrices and streamed one wave per row; with one
-table shared by B instances the backward sweep runs as one dgemm (fp64 MFMA
-through rocBLAS) over all instances.  Checked here:
+table shared by B instances every sweep's P . [v_1 .. v_B] contraction runs as
+one GEMM over all instances on the hand-written fp64 MFMA kernel
+(dense.hip dense_gemm_kernel; no library GEMM).  Checked here:
 
 * the generic fixtures (tests/golden/generic.npz: reference outputs for three
   non-grid MDPs, tools/gen_golden.py), forced onto the DENSE layout;
@@ -117,8 +118,7 @@ def test_random_dense_2048_vs_dense_oracle(dev, dense2048):
 
 def test_shared_table_gemm_backward(dev, dense2048, monkeypatch):
     """One dense table, 16 reward vectors: the backward sweep as one GEMM over all
-    instances (plan "dense-gemm") -- on the
-    hand-written fp64 MFMA kernel and on the library dgemm -- equals the
+    instances (plan "dense-gemm", the hand-written fp64 MFMA kernel) equals the
     per-instance streaming kernel and the oracle (instance 0 carries the
     fixture's reward)."""
     from irlmx import DeviceMDP, ops
@@ -130,10 +130,6 @@ def test_shared_table_gemm_backward(dev, dense2048, monkeypatch):
     tm = ops.terminal_mask(term, P.shape[0], batch=B, device=dev)
     assert ops.execution_plan(mdp, "backward")["shape"] == "dense-gemm"   # 16 instances: the MFMA kernel
     pi_gemm = ops.backward_maxent(mdp, rew, tm).cpu().numpy()            # hand-written fp64 MFMA kernel
-    monkeypatch.setenv("IRLMX_DENSE_GEMM_ENGINE", "rocblas")
-    pi_lib = ops.backward_maxent(mdp, rew, tm).cpu().numpy()             # library dgemm
-    monkeypatch.delenv("IRLMX_DENSE_GEMM_ENGINE")
-    close(pi_gemm, pi_lib, 1e-12, "mfma kernel vs rocblas")
     monkeypatch.setenv("IRLMX_DENSE_GEMM_MIN", "1000000")
     assert ops.execution_plan(mdp, "backward")["shape"] == "dense"
     pi_stream = ops.backward_maxent(mdp, rew, tm).cpu().numpy()
@@ -151,11 +147,11 @@ def test_dropin_accepts_dense_tables(dev, dense2048):
     close(S.value_iteration(P, r, 0.9), z["v"], 1e-12, "drop-in v")
 
 
-@pytest.mark.parametrize("n,batch", [(300, 5), (301, 3), (1040, 37)])
+@pytest.mark.parametrize("n,batch", [(300, 5), (301, 3), (302, 17), (1040, 37), (1037, 20)])
 def test_gemm_edges(dev, monkeypatch, n, batch):
     """The MFMA kernel's partial row / instance tiles (S not a multiple of 32, B not
-    a multiple of 16) and the library fallback (S % 4 != 0) against the streaming
-    kernel, forced onto the GEMM plan."""
+    a multiple of 16) and its K tail (S % 4 != 0, odd S: element-wise loads)
+    against the streaming kernel, forced onto the GEMM plan."""
     from irlmx import DeviceMDP, ops
     P, _, _, _ = O.random_dense_mdp(n, 3, seed=n)
     mdp = DeviceMDP.from_dense(P, device=dev, layout="dense").with_batch(batch)
@@ -199,3 +195,58 @@ def test_shared_table_gemm_soft_vi_and_vi(dev, dense2048, monkeypatch):
     assert int(g[2][0]) == int(z["k_s"]) and int(g[4][0]) == int(z["k_v"])
     close(g[0][0], z["cpi"], 1e-9, "soft pi vs oracle")
     close(g[3][0], z["v"], 1e-12, "v vs oracle")
+
+
+# (rows, n, batch, expected variant): every kernel variant dense_gemm_launch picks,
+# with partial tiles and K tails: {row tiles, instance tiles, waves, 16-byte loads}
+GEMM_SHAPES = [
+    (300, 300, 5, (1, 1, 8, 1)), (301, 301, 3, (1, 1, 8, 0)), (1040, 1037, 20, (1, 2, 8, 0)),
+    (4096, 4096, 16, (1, 1, 8, 1)), (4096, 4096, 64, (1, 4, 8, 1)), (8192, 4094, 16, (2, 1, 8, 1)),
+    (16384, 2049, 16, (2, 1, 4, 0)), (8192, 8192, 64, (2, 4, 8, 1)), (16384, 1030, 33, (2, 4, 4, 1)),
+    (2048 * 4, 2048, 16, (2, 1, 8, 1)),
+]
+
+
+@pytest.mark.parametrize("rows,n,batch,variant", GEMM_SHAPES)
+def test_dense_gemm_kernel_vs_torch(dev, rows, n, batch, variant):
+    """irlmx_dense_gemm (C = Z . M^T on v_mfma_f64_16x16x4_f64) against torch's
+    fp64 matmul of the same operands, for every variant of the kernel -- the
+    8-wave ST = 2 / NBT = 4 form with 128 KiB of LDS at S = 8192, B = 64 included
+    -- and K tails (n % 16 != 0, odd n); relative error within 1e-13."""
+    from irlmx import ops
+    assert ops.dense_gemm_variant(rows, n, batch) == variant
+    g = torch.Generator(device=dev).manual_seed(rows + n + batch)
+    m = torch.rand((rows, n), dtype=torch.float64, device=dev, generator=g)
+    z = torch.rand((batch, n), dtype=torch.float64, device=dev, generator=g)
+    c = ops.dense_gemm(m, z)
+    ref = z @ m.T
+    err = float((c - ref).abs().max() / ref.abs().max())
+    assert err <= 1e-13, (rows, n, batch, err)
+    # deterministic: a second call is bit-identical
+    assert torch.equal(ops.dense_gemm(m, z), c)
+
+
+def test_dense_8192_shared_table(dev):
+    """A dense S = 8192 table (2.1 GB of rows) shared by 64 instances: the VI
+    sweep (solver.py:40-50) on the GEMM plan (the stacked [4 S x S] products,
+    LDS-staged epilogue vectors) for a capped number of sweeps, against the
+    per-instance streaming kernel; also the LDS-staged streaming kernels at
+    S = 8192 with B > 1 (64 KiB of dynamic LDS)."""
+    from irlmx import DeviceMDP, ops
+    n, B = 8192, 64
+    P, _, _, _ = O.random_dense_mdp(n, 4, seed=8192)
+    mdp = DeviceMDP.from_dense(P, device=dev, layout="dense").with_batch(B)
+    del P
+    rew = np.random.default_rng(8192).uniform(0.0, 1.0, (B, n))
+    assert ops.execution_plan(mdp, "value_iteration")["shape"] == "dense-gemm"
+    v_g, k_g, st_g = ops.value_iteration(mdp, rew, 0.9, max_iter=6)
+    import os
+    os.environ["IRLMX_DENSE_GEMM_MIN"] = "1000000"
+    try:
+        assert ops.execution_plan(mdp, "value_iteration")["shape"] == "dense"
+        v_s, k_s, st_s = ops.value_iteration(mdp, rew, 0.9, max_iter=6)
+    finally:
+        del os.environ["IRLMX_DENSE_GEMM_MIN"]
+    assert k_g.tolist() == k_s.tolist() == [6] * B
+    close(v_g.cpu().numpy(), v_s.cpu().numpy(), 1e-12, "S=8192 VI gemm vs streaming")
+    torch.cuda.synchronize()

@@ -1,0 +1,114 @@
+"""Failure paths of the persistent shapes that need a device (cluster.hip).
+
+* Co-residency rejection (cluster_run): a plan whose workgroups cannot all be
+  resident at once is refused with IRLMX_EINVAL before launch.  Forced by
+  letting the planner believe in more CUs than the device has
+  (IRLMX_PLAN_CUS).
+* Exchange timeout: one workgroup leaves right after the co-residency
+  rendezvous (IRLMX_TEST_DROP_TILE) with a shortened exchange limit
+  (IRLMX_TEST_EXCHANGE_TIMEOUT_MS), so its neighbours' granule polls time out.
+  The call is rerun on the per-sweep shape -- bit-identical results, counted in
+  irlmx_counters' rerun_timeout -- or, with IRLMX_STRICT_EXCHANGE=1, fails
+  with IRLMX_EHIP and the timeout message.
+"""
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+torch = pytest.importorskip("torch")
+
+B = 4
+
+
+@pytest.fixture(scope="module")
+def dev():
+    import __graft_entry__ as g
+    g.build()
+    import irlmx
+    return irlmx.require_device()
+
+
+def make_world(dev, monkeypatch, size):
+    from irlmx import DeviceMDP, ops
+    for k in ("IRLMX_PLAN_CUS", "IRLMX_TEST_DROP_TILE", "IRLMX_TEST_EXCHANGE_TIMEOUT_MS", "IRLMX_STRICT_EXCHANGE",
+              "IRLMX_CLUSTER_R", "IRLMX_CLUSTER_G"):
+        monkeypatch.delenv(k, raising=False)
+    S = size * size
+    mdp = DeviceMDP.icy_gridworld(size, np.linspace(0.1, 0.3, B), device=dev)
+    rng = np.random.default_rng(4)
+    r = rng.uniform(0.0, 1.0, (B, S))
+    term = ops.terminal_mask([S - 1], S, batch=B, device=dev)
+    p0 = np.zeros((B, S))
+    p0[:, 0] = 1.0
+    return mdp, r, term, p0
+
+
+@pytest.fixture
+def world(dev, monkeypatch):
+    return make_world(dev, monkeypatch, 64)
+
+
+@pytest.fixture
+def world128(dev, monkeypatch):
+    """128x128: several tiles per instance in both passes, so every tile exchanges halos."""
+    return make_world(dev, monkeypatch, 128)
+
+
+def test_coresidency_rejection(world, monkeypatch):
+    from irlmx import _lib, ops
+    SIZE = 64
+    mdp, r, term, p0 = world
+    assert ops.execution_plan(mdp, "backward")["shape"] == "cluster"
+    monkeypatch.setenv("IRLMX_CLUSTER_R", "4")      # 16 tiles per instance
+    monkeypatch.setenv("IRLMX_CLUSTER_G", "2")
+    big = mdp.take(np.arange(B).repeat(8))         # 32 instances
+    monkeypatch.setenv("IRLMX_PLAN_CUS", "4096")   # planner: 256 instances per launch fit
+    plan = ops.execution_plan(big, "backward")
+    assert plan["C"] == 16 and plan["per_launch"] == 32, plan
+    n_cus = torch.cuda.get_device_properties(big.device).multi_processor_count
+    for call in (lambda: ops.backward_maxent(big, np.tile(r, (8, 1)), term.repeat(8, 1)),
+                 lambda: ops.forward_svf(big, np.tile(p0, (8, 1)), term.repeat(8, 1),
+                                         np.full((32, SIZE * SIZE, 4), 0.25))):
+        with pytest.raises(_lib.IrlmxError, match=rf"cluster: 512 workgroups cannot be co-resident \({n_cus}\)"):
+            call()
+    torch.cuda.synchronize()
+
+
+@pytest.mark.parametrize("op", ["backward", "forward"])
+def test_exchange_timeout_reruns_bit_identical(world128, monkeypatch, op):
+    from irlmx import _lib, ops
+    mdp, r, term, p0 = world128
+    for o in ("backward", "forward"):
+        assert ops.execution_plan(mdp, o)["C"] > 1
+    pi = ops.backward_maxent(mdp, r, term)
+    if op == "backward":
+        run = lambda: ops.backward_maxent(mdp, r, term)
+    else:
+        run = lambda: ops.forward_svf(mdp, p0, term, pi, max_iter=5000)
+    ref = run()
+    base = ops.counters()
+    monkeypatch.setenv("IRLMX_TEST_DROP_TILE", "1")
+    monkeypatch.setenv("IRLMX_TEST_EXCHANGE_TIMEOUT_MS", "50")
+    got = run()
+    after = ops.counters()
+    assert after["rerun_timeout"] == base["rerun_timeout"] + 1
+    assert after["sweep_calls"] == base["sweep_calls"] + 1
+    for g, e in zip(got if isinstance(got, tuple) else (got,), ref if isinstance(ref, tuple) else (ref,)):
+        assert torch.equal(g, e)
+    monkeypatch.setenv("IRLMX_STRICT_EXCHANGE", "1")
+    with pytest.raises(_lib.IrlmxError, match="halo exchange timed out"):
+        run()
+    torch.cuda.synchronize()
+
+
+def test_counters_record_persistent_launches(world):
+    from irlmx import ops
+    mdp, r, term, p0 = world
+    c0 = ops.counters()
+    pi = ops.backward_maxent(mdp, r, term)
+    ops.forward_svf(mdp, p0, term, pi, max_iter=100)
+    c1 = ops.counters()
+    assert c1["cluster_launches"] - c0["cluster_launches"] == 2
+    assert c1["sweep_calls"] == c0["sweep_calls"] and c1["rerun_not_resident"] == c0["rerun_not_resident"]

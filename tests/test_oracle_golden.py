@@ -220,9 +220,16 @@ def test_full_size_fixtures_consistent():
         slip = 0.1 + 0.2 * b / total
         assert float(z[f"{b}__slip"]) == slip
         n = size * size
-        e_f, p0, _ = demos.sample(O.stencil_row_val(O.icy_gridworld_csr(size, slip), size), size, [n - 1], 0,
-                                  n=200, seed=1234 + b)
+        rv = O.stencil_row_val(O.icy_gridworld_csr(size, slip), size)
+        e_f, p0, lens = demos.sample(rv, size, [n - 1], 0, n=200, seed=1234 + b)
         assert np.array_equal(e_f, z[f"{b}__e_f"]) and np.array_equal(p0, z[f"{b}__p0"])
+        # no demonstration of the bench workloads is cut: under the former cap of
+        # 64 * size steps (which produced the fixtures) every trajectory reached
+        # the terminal state, so the uncapped sampler regenerates them unchanged
+        cap = 64 * size
+        _, _, lens_c, cut = demos.sample(rv, size, [n - 1], 0, n=200, seed=1234 + b, max_len=cap,
+                                         with_truncated=True)
+        assert cut == 0 and np.array_equal(lens_c, lens) and int(lens.max()) < cap, (cfg, int(lens.max()))
     z = load_golden("dense2048")
     P, r, term, p0 = O.random_dense_mdp()
     assert np.array_equal(np.array([P.sum(), P[::7, ::5, :].sum(), P[-1, -1, -1]]), z["P_check"])
@@ -240,3 +247,20 @@ def test_full_size_fixtures_consistent():
         theta = theta * np.exp(0.2 / (1 + k) * (e_f - svf))
         assert kf == res["k_f"][k]
         assert np.max(np.abs(theta - res["theta"][k])) <= 1e-12 * np.max(np.abs(theta))
+
+
+def test_demos_truncation_reported():
+    """irlmx.demos.sample samples until terminal like the reference
+    (trajectory.py:76); a cap that cuts trajectories raises, or is counted."""
+    import numpy as np
+    import pytest
+    from irlmx import demos
+    size, n = 8, 64
+    rv = O.stencil_row_val(O.icy_gridworld_csr(size, 0.2), size)
+    _, _, lens = demos.sample(rv, size, [n - 1], 0, n=20, seed=3)
+    assert int(lens.min()) >= 2 * (size - 1)          # Manhattan distance from state 0 to the goal
+    with pytest.raises(demos.TruncatedDemonstrations):
+        demos.sample(rv, size, [n - 1], 0, n=20, seed=3, max_len=5)
+    e_f, _, lens5, cut = demos.sample(rv, size, [n - 1], 0, n=20, seed=3, max_len=5, on_truncate="allow",
+                                      with_truncated=True)
+    assert cut == 20 and int(lens5.max()) == 5 and abs(e_f.sum() - 6.0) < 1e-12   # 5 steps + the cut state

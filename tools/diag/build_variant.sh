@@ -8,4 +8,4 @@ name=$1; shift
 mkdir -p "$ROOT/build/$name"
 cd "$ROOT/irl-maxent_amd"
 /opt/rocm/bin/hipcc -O3 -std=c++17 --offload-arch=gfx950 -shared -fPIC -Wall -ffp-contract=off "$@" \
-  -o "$ROOT/build/$name/libirlmx.so" csrc/*.hip -L/opt/rocm/lib -lrocblas
+  -o "$ROOT/build/$name/libirlmx.so" csrc/*.hip
