@@ -277,28 +277,48 @@ def config1_timings(device_runs=True):
     import maxent_oracle as O
     z = np.load(os.path.join(ROOT, "tests", "golden", "config1.npz"))
     P, feats = z["p_transition"], np.identity(25)
-    tjs, o = [], 0
-    for n in z["traj_lens"]:
-        tjs.append(O.Trajectory([tuple(int(v) for v in row) for row in z["traj_flat"][o:o + n]]))
-        o += n
+    rows = [[tuple(int(v) for v in row) for row in z["traj_flat"][o - n:o]]
+            for n, o in zip(z["traj_lens"], np.cumsum(z["traj_lens"]))]
     out = {"workload": "BASELINE config 1: src/main.py 5x5 IcyGridWorld, 200 demos, full runs to eps=1e-4",
            "cpu_cores": int(blas_threads())}
-    runs = {"irl": lambda m, opt: m.irl(P, feats, [24], tjs, opt, O.Constant(1.0)),
-            "irl_causal": lambda m, opt: m.irl_causal(P, feats, [24], tjs, opt, O.Constant(1.0), DISCOUNT)}
-    import maxent as M   # the device drop-in (irl-maxent_amd/maxent.py)
+    import maxent as M            # the device drop-in (irl-maxent_amd/maxent.py)
+    import trajectory as T        # the drop-in trajectory container (irl-maxent_amd/trajectory.py)
+    tjs_dev = [T.Trajectory(r) for r in rows]
+    tjs_cpu = [O.Trajectory(r) for r in rows]
+
+    class ExpSga:
+        """The caller's optimizer, as src/main.py passes one (optimizer.py:110-167 protocol:
+        reset / step, theta *= exp(lr_k * grad) in place, lr_k = 0.2 / (1 + k))."""
+
+        def __init__(self):
+            self.k, self.parameters = 0, None
+
+        def reset(self, parameters):
+            self.parameters, self.k = parameters, 0
+
+        def step(self, grad, *args, **kwargs):
+            lr = 0.2 / (1.0 + self.k)
+            self.k += 1
+            self.parameters *= np.exp(lr * grad)
+
+    def init(n):                  # optimizer.Constant(1.0)
+        return np.ones(n)
+
+    runs = {"irl": lambda m, opt, tjs: m.irl(P, feats, [24], tjs, opt, init),
+            "irl_causal": lambda m, opt, tjs: m.irl_causal(P, feats, [24], tjs, opt, init, DISCOUNT)}
     for name, fn in runs.items():
         rec = {}
         if device_runs:
-            fn(M, O.ExpSga(lr=O.linear_decay(0.2)))          # warm-up (table upload, kernel load)
-            opt = O.ExpSga(lr=O.linear_decay(0.2))
+            fn(M, ExpSga(), tjs_dev)                          # warm-up (table upload, kernel load)
+            opt = ExpSga()
             t0 = time.perf_counter()
-            fn(M, opt)
+            fn(M, opt, tjs_dev)
             rec["gpu_dropin_s"] = time.perf_counter() - t0
             rec["steps"] = opt.k
             rec["gpu_dropin_steps_per_s"] = opt.k / rec["gpu_dropin_s"]
         opt = O.ExpSga(lr=O.linear_decay(0.2))
         t0 = time.perf_counter()
-        _, k = fn(O, opt)                                    # the oracle's loops return (reward, steps)
+        _, k = fn(O, opt, tjs_cpu)                           # the oracle's loops return (reward, steps)
         rec["cpu_port_s"] = time.perf_counter() - t0
         rec["cpu_port_steps"] = k
         rec["cpu_port_steps_per_s"] = k / rec["cpu_port_s"]
@@ -486,11 +506,15 @@ def main(argv=None):
     irl = BatchedMaxEnt(mdp, e_f, p_0, terminal, causal=causal, discount=DISCOUNT if causal else None)
     plans = {"backward": ops.execution_plan(mdp, "soft_backward" if causal else "backward"),
              "forward": ops.execution_plan(mdp, "forward")}
-    # one-time costs (code-object loading of every kernel, allocator growth) out of
-    # every timed figure: one backward and a 16-sweep forward on the same tables
+    # one-time costs (code-object loading of every kernel -- the library's and the
+    # torch elementwise kernels of the update --, allocator growth) out of every
+    # timed figure: one backward, a 16-sweep forward and an update on the same tables
     prime = BatchedMaxEnt(mdp, e_f, p_0, terminal, causal=causal, discount=DISCOUNT if causal else None)
-    ops.forward_svf(mdp, prime.p_initial, prime.terminal, prime.backward(), max_iter=16)
-    del prime
+    svf_p, _, _ = ops.forward_svf(mdp, prime.p_initial, prime.terminal, prime.backward(), max_iter=16)
+    prime.update(svf_p)
+    prime.last_delta.cpu()
+    ops.counters()
+    del prime, svf_p
     torch.cuda.synchronize()
 
     def barrier():

@@ -115,13 +115,19 @@ def compare_steps(z, checked, steps, n_states, causal=False):
                     assert np.all(np.abs(got - ref) <= RTOL * np.abs(ref)), (b, "pi0 sums", got, ref)
                 else:
                     close(pi, z[key + "pi0"], (b, "pi0"))
-                    # argmax identical wherever the best action is not tied to 1e-9
-                    # (theta0 = 1 makes mirror-symmetric states exact ties)
+                    # argmax identical wherever the best action is not tied to 1e-9;
+                    # where it is (theta0 = 1 makes mirror-symmetric states exact
+                    # ties mathematically, and the last bit of either side decides),
+                    # the device's argmax is one of the tied best actions
                     ref = z[key + "pi0"]
                     top = np.sort(ref, axis=1)
-                    clear = top[:, -1] - top[:, -2] > 1e-9 * np.max(ref)
-                    bad = int(np.count_nonzero(np.argmax(pi, axis=1)[clear] != np.argmax(ref, axis=1)[clear]))
+                    tol = 1e-9 * np.max(ref)
+                    clear = top[:, -1] - top[:, -2] > tol
+                    am = np.argmax(pi, axis=1)
+                    bad = int(np.count_nonzero(am[clear] != np.argmax(ref, axis=1)[clear]))
                     assert bad == 0, (b, "argmax differs at", bad, "untied states")
+                    tied_ok = ref[np.arange(len(am)), am] >= top[:, -1] - tol
+                    assert tied_ok.all(), (b, "argmax outside the tied set at", int((~tied_ok).sum()), "states")
             for name in ("svf", "theta"):
                 vec = st[name][j]
                 ref = z[f"{key}{name}{i}"]
@@ -172,3 +178,33 @@ def test_config5_forward_converged_on_reference_policy(dev):
     svf, k, st = ops.forward_svf(mdp, p0, ops.terminal_mask([n - 1], n, device=dev), ref["pi"])
     assert int(k[0]) == int(z["fwd__k_f"]) == 615955 and int(st[0]) == 0
     close(svf[0].cpu().numpy(), z["fwd__svf"], "svf")
+
+
+def test_config3_timed_steps_plan_independent(dev):
+    """The bench's timed steps (6..25 of irl from theta0 = 1; fixtures pin steps
+    1-3) on the benchmarked B = 64 plan equal, bit for bit and step for step,
+    the same instances run alone on a different plan (B = 2: smaller tiles, more
+    tiles per instance): per-instance results do not depend on the plan that
+    computes them, so the timed region computes what the pinned steps do."""
+    from irlmx import DeviceMDP, demos, ops
+    from irlmx.batch import BatchedMaxEnt
+    from irlmx.shard import instance_slips
+    size, B, S = 128, 64, 128 * 128
+    slips = instance_slips(np.arange(B), B)
+    mdp = DeviceMDP.icy_gridworld(size, slips, device=dev)
+    rv = mdp.row_val.cpu().numpy()
+    e_f = np.empty((B, S))
+    p0 = np.empty((B, S))
+    for b in range(B):
+        e_f[b], p0[b], _ = demos.sample(rv[b], size, [S - 1], 0, n=200, seed=1234 + b)
+    pick = np.array([0, 63])
+    sub = mdp.take(pick)
+    assert plan_subset(ops.execution_plan(mdp, "backward"), C3_BWD_PLAN) == C3_BWD_PLAN
+    assert ops.execution_plan(sub, "backward")["C"] > C3_BWD_PLAN["C"]
+    full = BatchedMaxEnt(mdp, e_f, p0, [S - 1])
+    alone = BatchedMaxEnt(sub, e_f[pick], p0[pick], [S - 1])
+    for step in range(25):
+        full.step()
+        alone.step()
+        assert torch.equal(full.last_forward_sweeps[pick], alone.last_forward_sweeps), step
+        assert torch.equal(full.theta[pick], alone.theta), step

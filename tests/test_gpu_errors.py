@@ -63,15 +63,19 @@ def test_coresidency_rejection(world, monkeypatch):
     assert ops.execution_plan(mdp, "backward")["shape"] == "cluster"
     monkeypatch.setenv("IRLMX_CLUSTER_R", "4")      # 16 tiles per instance
     monkeypatch.setenv("IRLMX_CLUSTER_G", "2")
-    big = mdp.take(np.arange(B).repeat(8))         # 32 instances
-    monkeypatch.setenv("IRLMX_PLAN_CUS", "4096")   # planner: 256 instances per launch fit
+    # 72 instances x 16 tiles = 1,152 workgroups: more than any CU count x the at
+    # most 4 resident 512-thread workgroups per CU (32 waves) of this device
+    n = 72
+    big = mdp.take(np.arange(B).repeat(n // B))
+    monkeypatch.setenv("IRLMX_PLAN_CUS", "16384")  # planner: 1,024 instances per launch fit
     plan = ops.execution_plan(big, "backward")
-    assert plan["C"] == 16 and plan["per_launch"] == 32, plan
+    assert plan["C"] == 16 and plan["per_launch"] == n, plan
     n_cus = torch.cuda.get_device_properties(big.device).multi_processor_count
-    for call in (lambda: ops.backward_maxent(big, np.tile(r, (8, 1)), term.repeat(8, 1)),
-                 lambda: ops.forward_svf(big, np.tile(p0, (8, 1)), term.repeat(8, 1),
-                                         np.full((32, SIZE * SIZE, 4), 0.25))):
-        with pytest.raises(_lib.IrlmxError, match=rf"cluster: 512 workgroups cannot be co-resident \({n_cus}\)"):
+    assert 16 * n > 4 * n_cus
+    for call in (lambda: ops.backward_maxent(big, np.tile(r, (n // B, 1)), term.repeat(n // B, 1)),
+                 lambda: ops.forward_svf(big, np.tile(p0, (n // B, 1)), term.repeat(n // B, 1),
+                                         np.full((n, SIZE * SIZE, 4), 0.25))):
+        with pytest.raises(_lib.IrlmxError, match=r"cluster: 1152 workgroups cannot be co-resident \(\d+\)"):
             call()
     torch.cuda.synchronize()
 
