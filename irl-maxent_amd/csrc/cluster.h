@@ -91,11 +91,13 @@ __device__ inline void gran_store(__amdgpu_buffer_rsrc_t r, unsigned off, unsign
 // after `limit` ticks of s_memrealtime (100 MHz; default 20 s).  Every pending
 // load of a pass is in flight at once.
 constexpr unsigned long long kGatherTicks = 2000000000ull;
-template <int N>
+// (mask type M: 32-bit, or 64-bit for more than 32 entries)
+template <int N, typename M>
 __device__ inline bool gran_gather(__amdgpu_buffer_rsrc_t r, __amdgpu_buffer_rsrc_t rl, const unsigned (&off)[N],
-                                   unsigned want, unsigned tag, unsigned long long (&v)[N],
+                                   M want, unsigned tag, unsigned long long (&v)[N],
                                    unsigned long long limit = kGatherTicks) {
-  unsigned pending = want;
+  static_assert(N <= 8 * (int)sizeof(M), "gran_gather: mask too narrow");
+  M pending = want;
   const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
   while (pending) {
     u32x4 x[N];
@@ -107,7 +109,7 @@ __device__ inline bool gran_gather(__amdgpu_buffer_rsrc_t r, __amdgpu_buffer_rsr
     for (int k = 0; k < N; ++k)
       if (((pending >> k) & 1u) && x[k].y == tag && x[k].w == tag) {
         v[k] = ((unsigned long long)x[k].z << 32) | x[k].x;
-        pending &= ~(1u << k);
+        pending &= ~((M)1 << k);
       }
     if (!pending) break;
     if (__builtin_amdgcn_s_memrealtime() - t0 > limit) return false;

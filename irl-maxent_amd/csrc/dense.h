@@ -98,4 +98,38 @@ hipError_t dense_gemm_launch(const double* M, const double* Z, double* C, int R,
 // {ST row tiles, NBT instance tiles, waves, 16-byte loads} of the launch dense_gemm_launch makes
 void dense_gemm_variant(int R, int S, int B, int* out);
 
+// Persistent dense shape (dense_grid.hip): the forward / collapsed backward loop
+// in one launch, each workgroup holding rb rows of its instance's matrix in
+// registers (columns t + 512 j, j < cpt), values exchanged as tagged granules.
+constexpr int kDenseGridThreads = 512;
+struct DenseGridPlan {
+  int rb, cpt, bpi, xcd;  // rows per workgroup, columns per thread, workgroups per instance, XCD grouping
+};
+struct DenseGridArgs {
+  int S, A, B, shared;
+  const double* mat;          // forward: WT [B][S][S]; backward: M [B'][S][S]
+  const double* P;            // backward final sweep: [B'][A][S][S]
+  const double* vin;          // forward: p0 [B][S]; backward: reward [B][S]
+  const uint8_t* term;        // backward: terminal mask [B][S]
+  const int32_t* bad;         // forward: non-finite policy [B]
+  double eps;
+  long long max_iter;
+  int rescale;
+  double* out;                // forward: svf [B][S]; backward: pi [B][S][A]
+  int64_t* iters;
+  int32_t* status;
+  unsigned long long* gran;   // [B][2][S] x 16-byte granules
+  unsigned long long* xgran;  // [B][bpi] x 16-byte granules (XCC ids)
+  int* err;                   // [0] timeout (1) / not co-resident (4); [1..2] rendezvous
+  int rb, bpi, nb, xcd_group; // (set by dense_grid_run)
+  unsigned salt;
+  int n_resident;
+};
+// mode: kModeFwd / kModeBwd (cluster.h).  False when the rows do not fit in
+// registers at one workgroup per CU (IRLMX_DENSE_GRID=0 disables the shape,
+// IRLMX_DENSE_GRID_RB forces the rows per workgroup).
+bool dense_grid_plan(int mode, int S, int B, DenseGridPlan* out);
+// 0, kClusterNotResident (rerun per sweep; err words cleared) or an IRLMX_E* code
+int dense_grid_run(int mode, const DenseGridPlan& p, DenseGridArgs a, hipStream_t st);
+
 }  // namespace irlmx

@@ -32,6 +32,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <initializer_list>
+#include <type_traits>
 #include <vector>
 
 #include "cluster.h"
@@ -141,6 +142,8 @@ struct GridPlan {
   int spt, bpi, xcd;
 };
 static bool grid_plan(const Model& m, int op, GridPlan* out);
+// Persistent dense shape (dense_grid.hip) for this call, if it applies.
+static bool dense_grid(const Model& m, int op, DenseGridPlan* out);
 
 static Ws carve(const Model& m, int op, void* base) {
   Ws w;
@@ -169,12 +172,16 @@ static Ws carve(const Model& m, int op, void* base) {
   const bool cl = sweep && m.stencil && (op == IRLMX_OP_FORWARD || op == IRLMX_OP_BACKWARD);
   GridPlan gp{0, 0, 0};
   const bool gr = sweep && grid_plan(m, op, &gp);
+  DenseGridPlan dp{0, 0, 0, 0};
+  const bool dg = sweep && dense_grid(m, op, &dp);
   // cluster halo exchange: [B][2][S] and [B][3][H] 16-byte granule pairs;
-  // grid shape: [B][3][S] value and [B][3][bpi] block-delta granules
-  w.gran = (unsigned long long*)take(cl ? 2 * B * S * 16 : (gr ? 3 * B * S * 16 : 0));
-  w.sgran = (unsigned long long*)take(cl ? 3 * B * (size_t)m.H * 16 : (gr ? 4 * B * (size_t)gp.bpi * 16 : 0));
+  // grid shape: [B][3][S] value and [B][3][bpi] block-delta granules;
+  // dense grid shape: [B][2][S] value and [B][bpi] XCC-id granules
+  w.gran = (unsigned long long*)take(cl || dg ? 2 * B * S * 16 : (gr ? 3 * B * S * 16 : 0));
+  w.sgran = (unsigned long long*)take(cl ? 3 * B * (size_t)m.H * 16
+                                         : (gr ? 4 * B * (size_t)gp.bpi * 16 : (dg ? B * (size_t)dp.bpi * 16 : 0)));
   w.growth = (unsigned long long*)take(cl ? B * sizeof(unsigned long long) : 0);
-  w.err = (int*)take(cl || gr ? 4 * sizeof(int) : 0);
+  w.err = (int*)take(cl || gr || dg ? 4 * sizeof(int) : 0);
   w.total = off;
   return w;
 }
@@ -917,16 +924,17 @@ __global__ void __launch_bounds__(kGridThreads) bellman_grid_kernel(SoftArgs a, 
       const unsigned tag = salt | ((unsigned)k & 0xFFFFFu);
       const unsigned slot = (unsigned)(k % 3);
       unsigned off[SPT * K + 1];
-      unsigned want = 0;
+      using mask_t = typename std::conditional<(SPT * K + 1 > 32), unsigned long long, unsigned>::type;
+      mask_t want = 0;
 #pragma unroll
       for (int j = 0; j < SPT; ++j)
 #pragma unroll
         for (int kk = 0; kk < K; ++kk) {
           off[j * K + kk] = (slot * (unsigned)S + (unsigned)nb[j][kk]) * 16u;
-          want |= (ok[j] && kk < Kr ? 1u : 0u) << (j * K + kk);
+          want |= (mask_t)(ok[j] && kk < Kr ? 1u : 0u) << (j * K + kk);
         }
       off[SPT * K] = (slot * (unsigned)g.bpi + (unsigned)tid) * 16u;
-      want |= (tid < g.bpi ? 1u : 0u) << (SPT * K);
+      want |= (mask_t)(tid < g.bpi ? 1u : 0u) << (SPT * K);
       unsigned long long v[SPT * K + 1];
       if (!gran_gather<SPT * K + 1>(rg, rd, off, want, tag, v)) lflag = 1;
 #pragma unroll
@@ -1132,16 +1140,17 @@ __global__ void __launch_bounds__(kGridThreads) linear_grid_kernel(LinearGridArg
       const unsigned tag = salt | ((unsigned)(k + 1) & 0xFFFFFu);
       const unsigned slot = (unsigned)(k % 3);
       unsigned off[SPT * K + 1];
-      unsigned want = 0;
+      using mask_t = typename std::conditional<(SPT * K + 1 > 32), unsigned long long, unsigned>::type;
+      mask_t want = 0;
 #pragma unroll
       for (int j = 0; j < SPT; ++j)
 #pragma unroll
         for (int kk = 0; kk < K; ++kk) {
           off[j * K + kk] = (slot * (unsigned)S + (unsigned)nb[j][kk]) * 16u;
-          want |= (ok[j] && kk < Kr ? 1u : 0u) << (j * K + kk);
+          want |= (mask_t)(ok[j] && kk < Kr ? 1u : 0u) << (j * K + kk);
         }
       off[SPT * K] = (slot * (unsigned)g.bpi + (unsigned)tid) * 16u;
-      want |= (tid < g.bpi ? 1u : 0u) << (SPT * K);
+      want |= (mask_t)(tid < g.bpi ? 1u : 0u) << (SPT * K);
       unsigned long long v[SPT * K + 1];
       if (!gran_gather<SPT * K + 1>(rg, rd, off, want, tag, v)) lflag = 1;
 #pragma unroll
@@ -1243,11 +1252,21 @@ static void* bellman_grid_fn(int spt, int kmax) {
       case 1: return (void*)&bellman_grid_kernel<SOFT, 1, 8>;
       case 2: return (void*)&bellman_grid_kernel<SOFT, 2, 8>;
     }
+  } else if (kmax == 16 && spt == 1) {
+    return (void*)&bellman_grid_kernel<SOFT, 1, 16>;
   }
   return nullptr;
 }
-static int grid_kmax(const Model& m) { return m.K <= 5 ? 5 : (m.K <= 8 ? 8 : 0); }
-static int grid_kmax_fwd(const Model& m) { return m.Kc <= 5 ? 5 : (m.Kc <= 8 ? 8 : 0); }
+// slots per state the grid kernels hold in registers: the linear loops up to 32
+// (ELL rows / columns of generic sparse models), the Bellman loops up to 16
+// (their A x K weights)
+static int grid_kmax_of(int K, int cap) {
+  const int k = K <= 5 ? 5 : (K <= 8 ? 8 : (K <= 16 ? 16 : (K <= 32 ? 32 : 0)));
+  return k <= cap ? k : 0;
+}
+static int grid_kmax(const Model& m) { return grid_kmax_of(m.K, 16); }
+static int grid_kmax_lin(const Model& m) { return grid_kmax_of(m.K, 32); }
+static int grid_kmax_fwd(const Model& m) { return grid_kmax_of(m.Kc, 32); }
 
 template <int MODE>
 static void* linear_grid_fn(int spt, int kmax) {
@@ -1262,6 +1281,13 @@ static void* linear_grid_fn(int spt, int kmax) {
       case 1: return (void*)&linear_grid_kernel<MODE, 1, 8>;
       case 2: return (void*)&linear_grid_kernel<MODE, 2, 8>;
     }
+  } else if (kmax == 16) {
+    switch (spt) {
+      case 1: return (void*)&linear_grid_kernel<MODE, 1, 16>;
+      case 2: return (void*)&linear_grid_kernel<MODE, 2, 16>;
+    }
+  } else if (kmax == 32 && spt == 1) {
+    return (void*)&linear_grid_kernel<MODE, 1, 32>;
   }
   return nullptr;
 }
@@ -1271,7 +1297,7 @@ static void* grid_fn(const Model& m, int op, int spt) {
     case IRLMX_OP_SOFT_BACKWARD: return bellman_grid_fn<true>(spt, grid_kmax(m));
     case IRLMX_OP_VALUE_ITERATION: return bellman_grid_fn<false>(spt, grid_kmax(m));
     case IRLMX_OP_FORWARD: return linear_grid_fn<kModeFwd>(spt, grid_kmax_fwd(m));
-    case IRLMX_OP_BACKWARD: return linear_grid_fn<kModeBwd>(spt, grid_kmax(m));
+    case IRLMX_OP_BACKWARD: return linear_grid_fn<kModeBwd>(spt, grid_kmax_lin(m));
   }
   return nullptr;
 }
@@ -1297,8 +1323,8 @@ static bool grid_plan(const Model& m, int op, GridPlan* out) {
   if (op == IRLMX_OP_SOFT_BACKWARD || op == IRLMX_OP_VALUE_ITERATION) {
     if (m.A > kGridMaxActions || !grid_kmax(m)) return false;
   } else if (op == IRLMX_OP_FORWARD || op == IRLMX_OP_BACKWARD) {
-    // stencil grids run the cluster shape; ELL rows of at most 8 slots here
-    if (m.stencil || !(op == IRLMX_OP_FORWARD ? grid_kmax_fwd(m) : grid_kmax(m)) || m.A > kMaxActions) return false;
+    // stencil grids run the cluster shape; ELL rows / columns of at most 32 slots here
+    if (m.stencil || !(op == IRLMX_OP_FORWARD ? grid_kmax_fwd(m) : grid_kmax_lin(m)) || m.A > kMaxActions) return false;
   } else {
     return false;
   }
@@ -1563,10 +1589,34 @@ static bool dense_gemm(const Model& m) {
   return m.B >= 16 || (m.S >= 4096 && m.B >= 4);
 }
 
+// The persistent dense shape takes the forward and the collapsed backward
+// whenever the rows fit in registers at one workgroup per CU (dense_grid.hip);
+// a backward that the planner gives to the GEMM keeps it.
+static bool dense_grid(const Model& m, int op, DenseGridPlan* out) {
+  if (!m.dense || (op != IRLMX_OP_FORWARD && op != IRLMX_OP_BACKWARD)) return false;
+  if (op == IRLMX_OP_BACKWARD && dense_gemm(m)) return false;
+  return dense_grid_plan(op == IRLMX_OP_FORWARD ? kModeFwd : kModeBwd, m.S, m.B, out);
+}
+
+static DenseGridArgs dense_grid_args(const Model& m, const Ws& ws) {
+  DenseGridArgs a{};
+  a.S = m.S; a.A = m.A; a.B = m.B; a.shared = m.shared;
+  a.gran = ws.gran; a.xgran = ws.sgran; a.err = ws.err;
+  return a;
+}
+
 static int dense_backward(const Model& m, const double* reward, const uint8_t* terminal, int rescale,
                           double* p_action, int32_t* status, const Ws& ws, hipStream_t st) {
   const DenseView d = dense_view(m);
   const DenseBufs w = dense_bufs(ws);
+  DenseGridPlan dp;
+  if (dense_grid(m, IRLMX_OP_BACKWARD, &dp)) {  // one persistent launch, M's rows in registers
+    DenseGridArgs a = dense_grid_args(m, ws);
+    a.mat = m.col_val; a.P = m.row_val; a.vin = reward; a.term = terminal;
+    a.rescale = rescale; a.out = p_action; a.status = status;
+    const int rc = dense_grid_run(kModeBwd, dp, a, st);
+    if (rc != kClusterNotResident) return rc;  // else: the per-sweep shape below
+  }
   dense_bwd_init_launch(d, terminal, w, st);
   const long long collapsed = 2LL * m.S - 1;
   const bool gemm = dense_gemm(m);
@@ -1650,6 +1700,18 @@ extern "C" int irlmx_execution_plan(const irlmx_mdp* mdp, int32_t op, int64_t* p
     plan[8] = 1;
     return 0;
   }
+  DenseGridPlan dp;
+  if (dense_grid(m, op, &dp)) {
+    plan[0] = IRLMX_SHAPE_DENSE_GRID;
+    plan[1] = dp.rb;    // (the R column: matrix rows per workgroup)
+    plan[2] = dp.xcd;
+    plan[3] = dp.bpi;
+    plan[4] = m.B;
+    plan[5] = dp.cpt;   // columns per thread
+    plan[7] = kDenseGridThreads;
+    plan[8] = 1;
+    return 0;
+  }
   if (m.dense) {
     const bool gemm = op != IRLMX_OP_FORWARD && dense_gemm(m);
     plan[0] = gemm ? IRLMX_SHAPE_DENSE_GEMM : IRLMX_SHAPE_DENSE;
@@ -1690,6 +1752,14 @@ extern "C" int irlmx_forward_svf(const irlmx_mdp* mdp, const double* p_initial, 
     const DenseView d = dense_view(m);
     const DenseBufs w = dense_bufs(ws);
     dense_fwd_weights_launch(d, p_action, terminal, w, st);
+    DenseGridPlan dp;
+    if (dense_grid(m, IRLMX_OP_FORWARD, &dp)) {  // one persistent launch, WT's rows in registers
+      DenseGridArgs ga = dense_grid_args(m, ws);
+      ga.mat = ws.wgt; ga.vin = p_initial; ga.bad = ws.bad; ga.eps = eps; ga.max_iter = (long long)max_iter;
+      ga.out = svf; ga.iters = iterations; ga.status = status;
+      const int rc = dense_grid_run(kModeFwd, dp, ga, st);
+      if (rc != kClusterNotResident) return rc;  // else: the per-sweep shape below
+    }
     int rc = run_until_done(ws, m.B, st, [&](long long it, int r3) {
       dense_fwd_sweep_launch(d, p_initial, eps, (long long)max_iter, status, w, it, r3, st);
     });

@@ -26,7 +26,7 @@ def _workspace(mdp, op):
 
 
 PLAN_FIELDS = ("shape", "R", "G", "C", "per_launch", "spt", "layout", "threads", "launches", "lds_bytes")
-SHAPES = {0: "fused", 1: "cluster", 2: "sweep", 3: "dense", 4: "dense-gemm", 5: "grid"}
+SHAPES = {0: "fused", 1: "cluster", 2: "sweep", 3: "dense", 4: "dense-gemm", 5: "grid", 6: "dense-grid"}
 _OPS = {"backward": _lib.OP_BACKWARD, "forward": _lib.OP_FORWARD, "soft_backward": _lib.OP_SOFT_BACKWARD,
         "value_iteration": _lib.OP_VALUE_ITERATION}
 

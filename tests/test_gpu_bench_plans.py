@@ -208,3 +208,43 @@ def test_config3_timed_steps_plan_independent(dev):
         alone.step()
         assert torch.equal(full.last_forward_sweeps[pick], alone.last_forward_sweeps), step
         assert torch.equal(full.theta[pick], alone.theta), step
+
+
+def test_config4_full_vectors_plan_independent(dev):
+    """Config 4's benchmarked plan (B = 32: R=16 / G=8 / C=16, two sequential
+    launches) against instances 0 and 31 run alone (B = 2: a different tile
+    count per instance, one launch): the whole policy (65,536 x 4) and SVF
+    (65,536) vectors, sweep counts and theta equal bit for bit for two gradient
+    steps.  Complements test_config4_bench_plan_two_irl_steps, whose fixture holds
+    4,096 states per vector plus whole-vector sums; with
+    test_gpu_parity.py::test_width256_quads_bit_identical (B = 2 plan == per-sweep
+    shape) this ties every state of the bench's plan to the per-sweep shape."""
+    from irlmx import DeviceMDP, demos, ops
+    from irlmx.batch import BatchedMaxEnt
+    from irlmx.shard import instance_slips
+    size, B, S = 256, 32, 256 * 256
+    slips = instance_slips(np.arange(B), B)
+    mdp = DeviceMDP.icy_gridworld(size, slips, device=dev)
+    rv = mdp.row_val.cpu().numpy()
+    e_f = np.empty((B, S))
+    p0 = np.empty((B, S))
+    for b in range(B):
+        e_f[b], p0[b], _ = demos.sample(rv[b], size, [S - 1], 0, n=200, seed=1234 + b)
+    pick = np.array([0, 31])
+    sub = mdp.take(pick)
+    assert plan_subset(ops.execution_plan(mdp, "backward"), C4_BWD_PLAN) == C4_BWD_PLAN
+    assert ops.execution_plan(sub, "backward") != ops.execution_plan(mdp, "backward")
+    full = BatchedMaxEnt(mdp, e_f, p0, [S - 1])
+    alone = BatchedMaxEnt(sub, e_f[pick], p0[pick], [S - 1])
+    idx = torch.as_tensor(pick, device=dev)
+    for step in range(2):
+        print(f"[c4 cross-plan] step {step}", flush=True)
+        pi_f, pi_a = full.backward(), alone.backward()
+        assert torch.equal(pi_f.index_select(0, idx), pi_a), (step, "pi")
+        svf_f, k_f, st_f = full.forward(pi_f)
+        svf_a, k_a, st_a = alone.forward(pi_a)
+        assert torch.equal(svf_f.index_select(0, idx), svf_a), (step, "svf")
+        assert torch.equal(k_f.index_select(0, idx), k_a) and torch.equal(st_f.index_select(0, idx), st_a)
+        full.update(svf_f)
+        alone.update(svf_a)
+        assert torch.equal(full.theta[pick], alone.theta), (step, "theta")

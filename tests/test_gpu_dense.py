@@ -72,7 +72,10 @@ def test_generic_fixtures_on_dense_layout(dev):
     for c in [str(n) for n in z["names"]]:
         P = z[c + "__P"]
         mdp = DeviceMDP.from_dense(P, device=dev, layout="dense")
-        assert mdp.layout == _lib.LAYOUT_DENSE and ops.execution_plan(mdp, "forward")["shape"] == "dense"
+        assert mdp.layout == _lib.LAYOUT_DENSE
+        # forward / backward: the persistent dense shape (test_gpu_dense_grid.py); soft VI / VI per sweep
+        assert ops.execution_plan(mdp, "forward")["shape"] == "dense-grid"
+        assert ops.execution_plan(mdp, "soft_backward")["shape"] == "dense"
         term = [int(t) for t in z[c + "__terminal"]]
         got = run_all(mdp, z[c + "__reward"], term, z[c + "__p0"], dev)
         close(got["pi"], z[c + "__pi"], 1e-9, c + " pi")
@@ -102,7 +105,8 @@ def test_random_dense_2048_vs_dense_oracle(dev, dense2048):
     P, r, term, p0, z = dense2048
     mdp = DeviceMDP.from_dense(P, device=dev)     # picked automatically: rows are full
     assert mdp.layout == _lib.LAYOUT_DENSE
-    assert ops.execution_plan(mdp, "backward")["shape"] == "dense"
+    assert ops.execution_plan(mdp, "backward")["shape"] == "dense-grid"
+    assert ops.execution_plan(mdp, "value_iteration")["shape"] == "dense"
     got = run_all(mdp, r, term, p0, dev)
     close(got["pi"], z["pi"], 1e-9, "pi")
     assert np.argmax(got["pi"], axis=1).tolist() == np.argmax(z["pi"], axis=1).tolist()

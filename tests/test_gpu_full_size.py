@@ -257,3 +257,70 @@ def test_ell_grid_shape_at_128(dev, monkeypatch):
     assert rel_err(pi, pi_ref) <= RTOL
     svf_ref, k_ref = O.forward_svf_csr(mats, p0[0], [n - 1], pi, max_iter=3000)
     assert int(got[1][1][0]) == k_ref == 3000 and rel_err(got[1][0][0].cpu().numpy(), svf_ref) <= RTOL
+
+
+def random_sparse_mats(n, A, n_succ, seed, n_offsets=32):
+    """Per-action CSR matrices of a random sparse MDP: state s reaches n_succ
+    distinct targets (s + o) mod n, o drawn per state from one fixed set of
+    n_offsets random offsets (so no state has more than n_offsets sources), each
+    action a random distribution over a random subset of them."""
+    import scipy.sparse as sp
+    rng = np.random.default_rng(seed)
+    offsets = rng.choice(np.arange(1, n), n_offsets, replace=False)
+    pick = np.argsort(rng.random((n, n_offsets)), axis=1)[:, :n_succ]
+    tgt = np.sort((np.arange(n)[:, None] + offsets[pick]) % n, axis=1)
+    mats = []
+    for _ in range(A):
+        w = rng.random((n, n_succ)) * (rng.random((n, n_succ)) < 0.5)
+        w[np.arange(n), rng.integers(0, n_succ, n)] += 0.5  # at least one target per action
+        w /= w.sum(axis=1, keepdims=True)
+        mats.append(sp.csr_matrix((w.ravel(), tgt.ravel(), np.arange(0, n * n_succ + 1, n_succ)), shape=(n, n)))
+    return mats
+
+
+@pytest.mark.parametrize("n_succ,kmax", [(12, 16), (24, 32)])
+def test_ell_grid_shape_wide_rows(dev, monkeypatch, n_succ, kmax):
+    """Generic sparse models with 9-32 slots per state (S = 6000 > one CU): the
+    linear loops (backward, forward) on the persistent grid shape with 16 / 32
+    slots per state in registers, soft VI and VI there too up to 16 slots -- bit
+    for bit the per-sweep shape (IRLMX_GRID=0), and the backward and capped
+    forward within 1e-9 of the CSR oracle."""
+    from irlmx import ops
+    from irlmx.batch import terminal_reward
+    n, B = 6000, 2
+    mats = random_sparse_mats(n, 4, n_succ, seed=n_succ)
+    mdp = ell_model(mats, dev).with_batch(B)
+    assert 8 < mdp.k_row <= kmax and mdp.k_col <= 32, (mdp.k_row, mdp.k_col)
+    for op in ("backward", "forward"):
+        assert ops.execution_plan(mdp, op)["shape"] == "grid", op
+    for op in ("soft_backward", "value_iteration"):
+        assert ops.execution_plan(mdp, op)["shape"] == ("grid" if kmax == 16 else "sweep"), op
+    rng = np.random.default_rng(n_succ)
+    r = rng.uniform(0.0, 1.0, (B, n))
+    tm = ops.terminal_mask([n - 1], n, batch=B, device=dev)
+    p0 = np.zeros((B, n))
+    p0[:, 0] = 1.0
+    phi = terminal_reward([n - 1], n, B, dev)
+
+    def run():
+        pi = ops.backward_maxent(mdp, r, tm)
+        return (pi, ops.forward_svf(mdp, p0, tm, pi, max_iter=500), ops.soft_backward(mdp, r, phi, 0.7),
+                ops.value_iteration(mdp, r, 0.9))
+
+    got = run()
+    monkeypatch.setenv("IRLMX_GRID", "0")
+    assert ops.execution_plan(mdp, "forward")["shape"] == "sweep"
+    ref = run()
+    monkeypatch.delenv("IRLMX_GRID")
+
+    def bits(x):
+        return x.view(torch.int64) if x.dtype == torch.float64 else x
+
+    flat = lambda t: list(t) if isinstance(t, tuple) else [t]
+    for g_, r_ in zip(got, ref):
+        for x, y in zip(flat(g_), flat(r_)):
+            assert torch.equal(bits(x), bits(y))
+    pi = got[0][1].cpu().numpy()
+    assert rel_err(pi, O.backward_maxent_csr(mats, [n - 1], r[1])) <= RTOL
+    svf_ref, k_ref = O.forward_svf_csr(mats, p0[1], [n - 1], pi, max_iter=500)
+    assert int(got[1][1][1]) == k_ref and rel_err(got[1][0][1].cpu().numpy(), svf_ref) <= RTOL

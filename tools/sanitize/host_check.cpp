@@ -87,12 +87,12 @@ static irlmx_mdp dense(int s, int a, int b) {
 }
 
 static const int kCus = 256;
-static long long g_shapes[6];
+static long long g_shapes[7];
 
 // Invariants of one plan (include/irlmx.h, IRLMX_PLAN_LEN fields).
 static void check_plan(const irlmx_mdp& m, int op, const int64_t* p, const char* what) {
   const int64_t shape = p[0];
-  CHECK(shape >= IRLMX_SHAPE_FUSED && shape <= IRLMX_SHAPE_GRID, "%s: shape %lld", what, (long long)shape);
+  CHECK(shape >= IRLMX_SHAPE_FUSED && shape <= IRLMX_SHAPE_DENSE_GRID, "%s: shape %lld", what, (long long)shape);
   if (shape == IRLMX_SHAPE_FUSED) {
     CHECK(p[7] >= 64 && p[7] <= 1024 && p[7] % 64 == 0, "%s: fused threads %lld", what, (long long)p[7]);
     CHECK(p[5] * p[7] >= m.n_states, "%s: fused spt %lld x %lld < S %d", what, (long long)p[5], (long long)p[7],
@@ -119,6 +119,14 @@ static void check_plan(const irlmx_mdp& m, int op, const int64_t* p, const char*
     CHECK(p[5] * p[7] * p[3] >= m.n_states, "%s: grid covers %lld < S", what, (long long)(p[5] * p[7] * p[3]));
   } else if (shape == IRLMX_SHAPE_DENSE || shape == IRLMX_SHAPE_DENSE_GEMM) {
     CHECK(m.layout == IRLMX_LAYOUT_DENSE, "%s: dense shape for layout %d", what, m.layout);
+  } else if (shape == IRLMX_SHAPE_DENSE_GRID) {
+    const int64_t rb = p[1], bpi = p[3], cpt = p[5];
+    CHECK(m.layout == IRLMX_LAYOUT_DENSE && (op == IRLMX_OP_BACKWARD || op == IRLMX_OP_FORWARD), "%s", what);
+    CHECK(p[7] == 512 && p[4] == m.batch && p[8] == 1, "%s: dense grid threads %lld", what, (long long)p[7]);
+    CHECK(rb >= 4 && rb <= 64 && rb * cpt <= 64, "%s: dense grid rb %lld cpt %lld", what, (long long)rb,
+          (long long)cpt);
+    CHECK(cpt * 512 >= m.n_states && bpi == (m.n_states + rb - 1) / rb, "%s: dense grid covers", what);
+    CHECK(bpi * m.batch <= kCus, "%s: dense grid %lld x %d workgroups", what, (long long)bpi, m.batch);
   }
 }
 
@@ -131,7 +139,7 @@ static void plan_and_workspace(const irlmx_mdp& m, const char* tag) {
     const int rc = irlmx_execution_plan(&m, op, plan);
     CHECK(rc == 0, "%s: plan rc %d (%s)", what, rc, irlmx_last_error());
     if (rc == 0) check_plan(m, op, plan, what);
-    if (rc == 0 && plan[0] >= 0 && plan[0] < 6) ++g_shapes[plan[0]];
+    if (rc == 0 && plan[0] >= 0 && plan[0] < 7) ++g_shapes[plan[0]];
     if (op == IRLMX_OP_BACKWARD) {
       int64_t p2[IRLMX_PLAN_LEN];
       CHECK(irlmx_execution_plan(&m, op | IRLMX_PLAN_NO_RESCALE, p2) == 0, "%s: no-rescale plan", what);
@@ -271,14 +279,16 @@ int main() {
     return 1;
   }
   CHECK(g_shapes[IRLMX_SHAPE_CLUSTER] > 1000 && g_shapes[IRLMX_SHAPE_GRID] > 100 && g_shapes[IRLMX_SHAPE_FUSED] > 100 &&
-            g_shapes[IRLMX_SHAPE_DENSE_GEMM] > 0,
-        "every shape planned: fused %lld cluster %lld sweep %lld dense %lld gemm %lld grid %lld", g_shapes[0],
-        g_shapes[1], g_shapes[2], g_shapes[3], g_shapes[4], g_shapes[5]);
+            g_shapes[IRLMX_SHAPE_DENSE_GEMM] > 0 && g_shapes[IRLMX_SHAPE_DENSE] > 0 &&
+            g_shapes[IRLMX_SHAPE_DENSE_GRID] > 0,
+        "every shape planned: fused %lld cluster %lld sweep %lld dense %lld gemm %lld grid %lld dense-grid %lld",
+        g_shapes[0], g_shapes[1], g_shapes[2], g_shapes[3], g_shapes[4], g_shapes[5], g_shapes[6]);
   if (g_fail) {
     fprintf(stderr, "host_check: %d of %lld checks failed\n", g_fail, g_checks);
     return 1;
   }
   printf("host_check ok: %lld plans, %lld checks; shapes fused %lld cluster %lld sweep %lld dense %lld dense-gemm %lld "
-         "grid %lld\n", plans, g_checks, g_shapes[0], g_shapes[1], g_shapes[2], g_shapes[3], g_shapes[4], g_shapes[5]);
+         "grid %lld dense-grid %lld\n", plans, g_checks, g_shapes[0], g_shapes[1], g_shapes[2], g_shapes[3], g_shapes[4],
+         g_shapes[5], g_shapes[6]);
   return 0;
 }
