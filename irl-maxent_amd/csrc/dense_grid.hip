@@ -83,22 +83,69 @@ __device__ inline double wave_sum_f64(double v) {
   return v;
 }
 
-// wave_sum_f64 of N independent values, level by level (the N dependent
-// chains interleave instead of running one after another)
+// a + b for two 64-lane double vectors after a cross-half exchange
+// (v_permlane32_swap / v_permlane16_swap on both 32-bit halves): each lane ends
+// up with the sum, over itself and its partner (lane ^ 32 / lane ^ 16), of ONE
+// of the two rows -- which one, the lane's `marker` says (probe_swap)
+template <int HALF>
+__device__ inline double swap_sum(double a, double b) {
+  const long long x = __double_as_longlong(a), y = __double_as_longlong(b);
+  const unsigned xl = (unsigned)x, xh = (unsigned)(x >> 32), yl = (unsigned)y, yh = (unsigned)(y >> 32);
+  auto lo = HALF == 32 ? __builtin_amdgcn_permlane32_swap(xl, yl, false, false)
+                       : __builtin_amdgcn_permlane16_swap(xl, yl, false, false);
+  auto hi = HALF == 32 ? __builtin_amdgcn_permlane32_swap(xh, yh, false, false)
+                       : __builtin_amdgcn_permlane16_swap(xh, yh, false, false);
+  const double a2 = __longlong_as_double(((long long)hi[0] << 32) | (long long)lo[0]);
+  const double b2 = __longlong_as_double(((long long)hi[1] << 32) | (long long)lo[1]);
+  return a2 + b2;
+}
+// which of the two rows a lane holds after swap_sum<HALF> (0: the first operand's)
+template <int HALF>
+__device__ inline int probe_swap() {
+  auto p = HALF == 32 ? __builtin_amdgcn_permlane32_swap(0u, 1u, false, false)
+                      : __builtin_amdgcn_permlane16_swap(0u, 1u, false, false);
+  return (int)p[0];
+}
+
+// Transposed wave reduction of N row partials (N = 4, 8, 16): every exchange
+// level halves the rows a lane carries instead of reducing each row over all
+// 64 lanes (N = 8: 34 VALU instructions instead of 144) -- lane ^ 32 and
+// lane ^ 16 by permlane swaps (no selects), lane ^ 8 (row_ror:8) and lane ^ 7
+// (row_half_mirror) with the kept / sent row chosen by the lane's bit, then
+// plain butterflies over the lanes left.  On return v[0] holds the full sum of
+// row `row` in every lane of a group of 64 / N consecutive lanes.  Fixed order:
+// deterministic.
 template <int N>
-__device__ inline void wave_sums_f64(double (&v)[N]) {
+__device__ inline double rows_sum(double (&v)[N], int lane, int& row) {
+  static_assert(N == 4 || N == 8 || N == 16, "rows_sum: 4, 8 or 16 rows");
+  const int m32 = probe_swap<32>(), m16 = probe_swap<16>();
 #pragma unroll
-  for (int i = 0; i < N; ++i) v[i] += dpp_f64<0xB1, 0xF>(v[i]);
+  for (int i = 0; i < N / 2; ++i) v[i] = swap_sum<32>(v[i], v[i + N / 2]);
 #pragma unroll
-  for (int i = 0; i < N; ++i) v[i] += dpp_f64<0x4E, 0xF>(v[i]);
+  for (int i = 0; i < N / 4; ++i) v[i] = swap_sum<16>(v[i], v[i + N / 4]);
+  row = m32 * (N / 2) + m16 * (N / 4);
+  if constexpr (N >= 8) {  // lane ^ 8: bit 3 picks the row kept
+    const bool b3 = (lane >> 3) & 1;
 #pragma unroll
-  for (int i = 0; i < N; ++i) v[i] += dpp_f64<0x141, 0xF>(v[i]);
-#pragma unroll
-  for (int i = 0; i < N; ++i) v[i] += dpp_f64<0x140, 0xF>(v[i]);
-#pragma unroll
-  for (int i = 0; i < N; ++i) v[i] += dpp_f64<0x142, 0xA>(v[i]);
-#pragma unroll
-  for (int i = 0; i < N; ++i) v[i] += dpp_f64<0x143, 0xC>(v[i]);
+    for (int i = 0; i < N / 8; ++i) {
+      const double send = b3 ? v[i] : v[i + N / 8], keep = b3 ? v[i + N / 8] : v[i];
+      v[i] = keep + dpp_f64<0x128, 0xF>(send);  // row_ror:8
+    }
+    row += b3 ? N / 8 : 0;
+  } else {
+    v[0] += dpp_f64<0x128, 0xF>(v[0]);
+  }
+  if constexpr (N == 16) {  // lane ^ 7 (same bits 3..5): bit 2 picks the row kept
+    const bool b2 = (lane >> 2) & 1;
+    const double send = b2 ? v[0] : v[1], keep = b2 ? v[1] : v[0];
+    v[0] = keep + dpp_f64<0x141, 0xF>(send);  // row_half_mirror
+    row += b2 ? 1 : 0;
+  } else {
+    v[0] += dpp_f64<0x141, 0xF>(v[0]);
+  }
+  v[0] += dpp_f64<0x4E, 0xF>(v[0]);  // quad_perm [2,3,0,1]
+  v[0] += dpp_f64<0xB1, 0xF>(v[0]);  // quad_perm [1,0,3,2]
+  return v[0];
 }
 
 __device__ inline int dg_finish_status(double delta, double eps) {
@@ -206,8 +253,8 @@ __global__ void __launch_bounds__(kDG) dense_grid_kernel(DenseGridArgs a) {
   // computed from v_k before the loop test on v_k is known (both go through
   // LDS at the same barrier); when the test stops the loop they are dropped.
   for (;;) {
-    // row dots in chunks of up to 16 rows (bounded live registers), each chunk's
-    // wave sums interleaved
+    // row dots in chunks of up to 16 rows (bounded live registers), each chunk
+    // reduced over the wave by rows_sum
     constexpr int CH = RB < 16 ? RB : 16;
 #pragma unroll
     for (int r0 = 0; r0 < RB; r0 += CH) {
@@ -218,11 +265,9 @@ __global__ void __launch_bounds__(kDG) dense_grid_kernel(DenseGridArgs a) {
 #pragma unroll
         for (int j = 0; j < CPT; ++j) acc[r] = fma(m[r0 + r][j], cur[j], acc[r]);
       }
-      wave_sums_f64<CH>(acc);
-      if (lane == kWave - 1) {
-#pragma unroll
-        for (int r = 0; r < CH; ++r) red[wave][r0 + r] = acc[r];
-      }
+      int row;
+      const double sum = rows_sum<CH>(acc, lane, row);
+      if ((lane & (kWave / CH - 1)) == 0) red[wave][r0 + row] = sum;
     }
     __syncthreads();
     if (k > 0) {
@@ -383,25 +428,35 @@ bool dense_grid_plan(int mode, int S, int B, DenseGridPlan* out) {
   const int f_cus = env_int("IRLMX_PLAN_CUS", 0);
   const int cus = f_cus > 0 ? f_cus : device_cus();
   if (cus <= 0) return false;
-  // the fewest rows per workgroup (most workgroups) at one workgroup per CU:
-  // a row dot costs a wave sum per row, the gather a whole vector per workgroup
-  for (int rb = 4; rb <= 64; rb *= 2) {
-    if (forced > 0 && rb != forced) continue;
-    void* fn = dense_grid_fn(mode, rb, cpt);
-    if (!fn) continue;
-    const int bpi = (S + rb - 1) / rb;
-    if ((long long)bpi * B > cus) continue;
-    const int cap = capacity(fn);
-    if ((long long)bpi * B > cap) continue;
-    // XCD groups (each instance within one XCD) from 8 instances on, as the grid
-    // shape; IRLMX_DENSE_GRID_XCD=1 asks for them at any batch (then only row
-    // blockings that fit one XCD qualify), 0 never
-    const int fx = env_int("IRLMX_DENSE_GRID_XCD", -1);
-    const bool fits = cap >= 8 && bpi <= kDG && (long long)((B + 7) / 8) * bpi <= cus / 8;
-    if (fx == 1 && !fits) continue;
-    const bool xcd = env_int("IRLMX_XCD_GROUP", 1) != 0 && fits && (fx == 1 || (fx != 0 && B >= 8));
-    *out = DenseGridPlan{rb, cpt, bpi, xcd ? 1 : 0};
-    return true;
+  // XCD groups: every instance's workgroups within one XCD (plain stores, one
+  // L2; a group of 8 instances per round of the 8 XCDs).  IRLMX_DENSE_GRID_XCD
+  // = 1 insists on them, 0 never takes them.
+  const int fx = env_int("IRLMX_DENSE_GRID_XCD", -1);
+  const bool xcd_ok = env_int("IRLMX_XCD_GROUP", 1) != 0 && fx != 0;
+  // Measured preference (profiles/r03_dense_grid_bench.txt, tools/diag/dense_grid_bench.py):
+  //  1. XCD-grouped, the fewest rows per workgroup that fit one XCD per instance
+  //     group (0.4-0.5 us per sweep below the spread form at equal rows);
+  //  2. spread over the chip at >= 8 rows and <= 128 workgroups per instance
+  //     (the gather costs a whole vector per workgroup; rows are cheap with the
+  //     transposed reduction), else any row count that fits one workgroup per CU.
+  int pref = 8;
+  while (pref < 64 && (S + pref - 1) / pref > 128) pref *= 2;
+  for (int pass = 0; pass < 3; ++pass) {
+    if (pass == 0 && !xcd_ok) continue;
+    if (pass > 0 && fx == 1) break;
+    for (int rb = pass == 1 ? pref : 4; rb <= 64; rb *= 2) {
+      if (forced > 0 && rb != forced) continue;
+      void* fn = dense_grid_fn(mode, rb, cpt);
+      if (!fn) continue;
+      const int bpi = (S + rb - 1) / rb;
+      if ((long long)bpi * B > cus) continue;
+      const int cap = capacity(fn);
+      if ((long long)bpi * B > cap) continue;
+      const bool fits = cap >= 8 && bpi <= kDG && (long long)((B + 7) / 8) * bpi <= cus / 8;
+      if (pass == 0 && !fits) continue;
+      *out = DenseGridPlan{rb, cpt, bpi, pass == 0 ? 1 : 0};
+      return true;
+    }
   }
   return false;
 }

@@ -103,14 +103,14 @@ def test_dense_grid_vs_per_sweep(dev, monkeypatch, n, A, batch, shared):
 
 def test_dense_grid_vs_oracle_2048(dev):
     """The seeded S = 2048 dense MDP (tests/golden/dense2048.npz, the dense oracle's
-    outputs): backward and forward on the dense grid shape (8 rows x 4 columns per
-    thread, 256 workgroups), sweep count identical, 1e-9."""
+    outputs): backward and forward on the dense grid shape (16 rows x 4 columns per
+    thread, 128 workgroups), sweep count identical, 1e-9."""
     from irlmx import DeviceMDP, ops
     z = load_golden("dense2048")
     P, r, term, p0 = O.random_dense_mdp()
     mdp = DeviceMDP.from_dense(P, device=dev)
     plan = ops.execution_plan(mdp, "backward")
-    assert (plan["shape"], plan["R"], plan["spt"], plan["C"]) == ("dense-grid", 8, 4, 256)
+    assert (plan["shape"], plan["R"], plan["spt"], plan["C"], plan["G"]) == ("dense-grid", 16, 4, 128, 0)
     tm = ops.terminal_mask(term, 2048, device=dev)
     pi = ops.backward_maxent(mdp, r, tm)[0].cpu().numpy()
     assert rel(pi, z["pi"]) <= 1e-9
@@ -128,8 +128,7 @@ def test_dense_grid_every_instantiation(dev, monkeypatch, n, rb, xcd):
     ragged last workgroup), IRLMX_DENSE_GRID_XCD=1 one instance's workgroups onto
     one XCD (plain stores): backward and a 400-sweep forward against the per-sweep
     dense shape, and against the dense oracle up to S = 700."""
-    if xcd:
-        monkeypatch.setenv("IRLMX_DENSE_GRID_XCD", "1")
+    monkeypatch.setenv("IRLMX_DENSE_GRID_XCD", str(xcd))
     from irlmx import ops
     mdp, (P,) = dense_model(dev, n, 3, 1, True, seed=7 * n)
     r = np.random.default_rng(rb).uniform(0.0, 1.0, n)
@@ -148,6 +147,7 @@ def test_dense_grid_every_instantiation(dev, monkeypatch, n, rb, xcd):
     assert ops.execution_plan(mdp, "forward")["R"] == rb
     (pi, svf, k, st), (pi_s, svf_s, k_s, st_s) = both_shapes(monkeypatch, run)
     monkeypatch.delenv("IRLMX_DENSE_GRID_RB")
+    monkeypatch.delenv("IRLMX_DENSE_GRID_XCD")
     assert rel(pi, pi_s) <= RTOL and (k, st) == (k_s, st_s)
     assert rel(svf, svf_s) <= 1e-11
     if n <= 700:
@@ -155,6 +155,20 @@ def test_dense_grid_every_instantiation(dev, monkeypatch, n, rb, xcd):
         svf_ref, k_ref = O.forward_svf(P, p0, [n - 1], pi, max_iter=400)
         assert k == k_ref and st == (0 if k_ref < 400 else 2)
         assert rel(svf, svf_ref) <= 1e-9
+
+
+@pytest.mark.parametrize("n,batch,plan", [(256, 1, (8, 32, 1)), (512, 2, (16, 32, 1)), (1024, 1, (32, 32, 1)),
+                                          (1024, 8, (32, 32, 1)), (512, 8, (16, 32, 1)), (2048, 1, (16, 128, 0)), (2048, 2, (16, 128, 0))])
+def test_dense_grid_planner(dev, n, batch, plan):
+    """The planner's measured preference: one XCD per instance
+    group at the fewest rows per workgroup that fit, else >= 8 rows and at most
+    128 workgroups per instance spread over the chip; (rows, workgroups per
+    instance, XCD-grouped)."""
+    from irlmx import ops
+    mdp, _ = dense_model(dev, n, 2, batch, True, seed=1)
+    for op in ("forward", "backward"):
+        p = ops.execution_plan(mdp, op)
+        assert (p["shape"], p["R"], p["C"], p["G"]) == ("dense-grid",) + plan, (op, p)
 
 
 def test_dense_grid_loop_edges(dev, monkeypatch):

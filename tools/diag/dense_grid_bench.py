@@ -35,7 +35,7 @@ for S in sizes:
         pi = ops.backward_maxent(mdp, r, tm)
         variants = [("per-sweep", {"IRLMX_DENSE_GRID": "0"}), ("planner", {})]
         for rb in [int(x) for x in os.environ.get("RBS", "4,8,16,32,64").split(",")]:
-            variants.append((f"rb={rb}", {"IRLMX_DENSE_GRID_RB": str(rb)}))
+            variants.append((f"rb={rb}", {"IRLMX_DENSE_GRID_RB": str(rb), "IRLMX_DENSE_GRID_XCD": "0"}))
             variants.append((f"rb={rb} xcd", {"IRLMX_DENSE_GRID_RB": str(rb), "IRLMX_DENSE_GRID_XCD": "1"}))
         for name, env in variants:
             for k in ("IRLMX_DENSE_GRID", "IRLMX_DENSE_GRID_RB", "IRLMX_DENSE_GRID_XCD"):
