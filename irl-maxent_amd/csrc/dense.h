@@ -104,18 +104,23 @@ void dense_gemm_variant(int R, int S, int B, int* out);
 constexpr int kDenseGridThreads = 512;
 struct DenseGridPlan {
   int rb, cpt, bpi, xcd;  // rows per workgroup, columns per thread, workgroups per instance, XCD grouping
+  int at;                 // soft VI / VI: actions compiled (4 or 8), else 0
 };
 struct DenseGridArgs {
   int S, A, B, shared;
   const double* mat;          // forward: WT [B][S][S]; backward: M [B'][S][S]
   const double* P;            // backward final sweep: [B'][A][S][S]
-  const double* vin;          // forward: p0 [B][S]; backward: reward [B][S]
+  const double* vin;          // forward: p0 [B][S]; backward, soft VI, VI: reward [B][S]
   const uint8_t* term;        // backward: terminal mask [B][S]
   const int32_t* bad;         // forward: non-finite policy [B]
+  const double* phi;          // soft VI: terminal reward [B][S]
+  double discount;            // soft VI / VI
+  int average;                // VI: mean over actions (solver.py:99) instead of the max
+  double* value;              // soft VI / VI: value out [B][S] (optional for soft VI)
   double eps;
   long long max_iter;
   int rescale;
-  double* out;                // forward: svf [B][S]; backward: pi [B][S][A]
+  double* out;                // forward: svf [B][S]; backward, soft VI: pi [B][S][A]
   int64_t* iters;
   int32_t* status;
   unsigned long long* gran;   // [B][2][S] x 16-byte granules
@@ -131,5 +136,10 @@ struct DenseGridArgs {
 bool dense_grid_plan(int mode, int S, int B, DenseGridPlan* out);
 // 0, kClusterNotResident (rerun per sweep; err words cleared) or an IRLMX_E* code
 int dense_grid_run(int mode, const DenseGridPlan& p, DenseGridArgs a, hipStream_t st);
+// Soft VI / VI (maxent.py:326-341, solver.py:40-50 / 95-100) of a DENSE model in
+// one persistent launch: each workgroup holds the A rows P_a of its rb states
+// (A <= 8; A * rb * cpt <= 64 doubles per thread)
+bool dense_bellman_grid_plan(int S, int B, int A, DenseGridPlan* out);
+int dense_bellman_grid_run(bool soft, const DenseGridPlan& p, DenseGridArgs a, hipStream_t st);
 
 }  // namespace irlmx

@@ -41,6 +41,7 @@
 
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <atomic>
 #include <cstdlib>
 
@@ -151,6 +152,54 @@ __device__ inline double rows_sum(double (&v)[N], int lane, int& row) {
 __device__ inline int dg_finish_status(double delta, double eps) {
   if (delta != delta) return IRLMX_NONFINITE;
   return delta > eps ? IRLMX_MAXITER : IRLMX_OK;
+}
+
+}  // namespace
+
+namespace {
+
+// This workgroup's instance and index within it; false for the padding
+// workgroups of an XCD-grouped grid.  XCD grouping (as the grid shape):
+// workgroups are dealt round-robin over the 8 XCDs, so the workgroups of
+// instance g + 8 j all come from XCD group g and its granules stay in one L2.
+__device__ inline bool dg_place(const DenseGridArgs& a, int& b, int& blk) {
+  int lin = blockIdx.x;
+  if (a.xcd_group) {
+    const int grp = blockIdx.x % 8, kk = blockIdx.x / 8;
+    const int il = grp + 8 * (kk / a.bpi);
+    if (il >= a.nb) return false;
+    lin = il * a.bpi + kk % a.bpi;
+  }
+  b = lin / a.bpi;
+  blk = lin % a.bpi;
+  return true;
+}
+
+// Plain stores (kept in the XCD's L2) when every workgroup of the instance runs
+// on one XCD -- found by exchanging XCC ids once; -1 when that exchange timed
+// out.  `scratch` is a workgroup array of kDGWaves words.
+__device__ inline int dg_plain(const DenseGridArgs& a, int b, int blk, unsigned salt,
+                               unsigned long long* scratch, int* lflag) {
+  if (!a.xcd_group) return 0;
+  const int tid = threadIdx.x, wave = tid / kWave, lane = tid & (kWave - 1);
+  const __amdgpu_buffer_rsrc_t rx = gran_rsrc(a.xgran + (size_t)b * 2 * a.bpi, 16u * (unsigned)a.bpi);
+  unsigned xcc;
+  asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
+  xcc &= 0xFu;
+  const unsigned htag = salt | 0xFFFFFu;
+  if (tid == 0) gran_store(rx, (unsigned)blk * 16u, xcc, htag, false);
+  unsigned off[1] = {(unsigned)(tid < a.bpi ? tid : 0) * 16u};
+  unsigned long long v[1] = {xcc};
+  if (!gran_gather<1>(rx, rx, off, tid < a.bpi ? 1u : 0u, htag, v)) *lflag = 1;
+  const unsigned long long diff = wave_or_u64(tid < a.bpi ? (v[0] ^ xcc) : 0ull);
+  if (lane == 0) scratch[wave] = diff;
+  __syncthreads();
+  if (*lflag) return -1;
+  unsigned long long any = 0ull;
+#pragma unroll
+  for (int i = 0; i < kDGWaves; ++i) any |= scratch[i];
+  __syncthreads();
+  return any == 0ull ? 1 : 0;
 }
 
 }  // namespace
@@ -375,6 +424,159 @@ __global__ void __launch_bounds__(kDG) dense_grid_kernel(DenseGridArgs a) {
   if (blk == 0 && tid == 0) a.status[b] = IRLMX_OK;
 }
 
+// Soft VI / VI of a DENSE model (the per-sweep dense_bellman_sweep_kernel's
+// statements, maxent.py:326-341, solver.py:40-50 / 95-100), one launch: the
+// workgroup holds the A rows P_a[s, :] of each of its RB states (AT >= A
+// compiled; the rows of actions >= A are zero), so a sweep is AT * RB row dots
+// (the transposed wave reduction in chunks of 16), then thread r folds its
+// state's A dots into the new value -- soft: v = phi, v = softmax(v, r + g dot_a)
+// in action order; VI: max / mean of g dot_a, plus r -- and publishes it.  The
+// loop test max|v_k - v_{k-1}| comes from the gathered vector, as in the
+// forward.  After the stop at v_k: value = v_k and, soft, pi = exp(q - v_k)
+// with q from the sweep that produced v_k (maxent.py:341).
+template <bool SOFT, int AT, int RB, int CPT>
+__global__ void __launch_bounds__(kDG) dense_bellman_grid_kernel(DenseGridArgs a) {
+  constexpr int K = AT * RB;  // matrix rows per workgroup: (action, state)
+  static_assert(K % 16 == 0 && K <= 64, "dense_bellman_grid_kernel: 16, 32, 48 or 64 rows");
+  const int S = a.S, A = a.A;
+  int b, blk;
+  if (!dg_place(a, b, blk)) return;
+  const int tid = threadIdx.x, wave = tid / kWave, lane = tid & (kWave - 1);
+  __shared__ int resident, lflag;
+  __shared__ double red[kDGWaves][K];
+  __shared__ unsigned long long mred[2][kDGWaves];
+  if (tid == 0) {
+    resident = coresident(a.err + 1, a.n_resident) ? 1 : 0;
+    lflag = 0;
+  }
+  __syncthreads();
+  if (!resident) {
+    if (tid == 0) atomicOr(a.err, kErrNotResident);
+    return;
+  }
+  const int row0 = blk * RB;
+  const size_t tab = a.shared ? 0 : (size_t)b;
+  const double* Pb = a.P + tab * (size_t)A * S * S;
+  double m[K][CPT];  // row act * RB + r: P_act[row0 + r, columns tid + kDG * j]
+#pragma unroll
+  for (int act = 0; act < AT; ++act)
+#pragma unroll
+    for (int r = 0; r < RB; ++r)
+#pragma unroll
+      for (int j = 0; j < CPT; ++j) {
+        const int row = row0 + r, c = tid + kDG * j;
+        m[act * RB + r][j] =
+            (act < A && row < S && c < S) ? Pb[((size_t)act * S + row) * S + c] : 0.0;
+      }
+  // thread r < RB: its state's reward and terminal reward, last value and q
+  const bool owner = tid < RB && row0 + tid < S;
+  const size_t srow = (size_t)b * S + row0 + (owner ? tid : 0);
+  const double rr = owner ? a.vin[srow] : 0.0;
+  const double ph = (SOFT && owner) ? a.phi[srow] : 0.0;
+  const double v0 = SOFT ? -1e200 : 0.0;  // maxent.py:323 / solver.py:32
+  double vkeep = v0, qkeep[AT];
+#pragma unroll
+  for (int act = 0; act < AT; ++act) qkeep[act] = 0.0;
+  double cur[CPT];
+  unsigned off0[CPT];
+  unsigned want = 0;
+#pragma unroll
+  for (int j = 0; j < CPT; ++j) {
+    const int c = tid + kDG * j;
+    off0[j] = (unsigned)(c < S ? c : S - 1) * 16u;
+    want |= (c < S ? 1u : 0u) << j;
+    cur[j] = c < S ? v0 : 0.0;
+  }
+  const __amdgpu_buffer_rsrc_t rg = gran_rsrc(a.gran + (size_t)b * 4 * S, 32u * (unsigned)S);
+  const unsigned salt = (a.salt & 0xFFFu) << 20;
+  const int pl = dg_plain(a, b, blk, salt, &mred[0][0], &lflag);
+  if (pl < 0) {
+    if (tid == 0) atomicOr(a.err, 1);
+    return;
+  }
+  const bool plain = pl == 1;
+  double delta = 0.0;
+  long long k = 0;  // sweeps done: cur = v_k
+  for (;;) {
+#pragma unroll
+    for (int r0 = 0; r0 < K; r0 += 16) {
+      double acc[16];
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        acc[r] = 0.0;
+#pragma unroll
+        for (int j = 0; j < CPT; ++j) acc[r] = fma(m[r0 + r][j], cur[j], acc[r]);
+      }
+      int row;
+      const double sum = rows_sum<16>(acc, lane, row);
+      if ((lane & 3) == 0) red[wave][r0 + row] = sum;
+    }
+    __syncthreads();
+    if (k > 0) {
+      if (lflag) {
+        if (tid == 0) atomicOr(a.err, 1);
+        return;
+      }
+      unsigned long long mx = 0ull;
+#pragma unroll
+      for (int i = 0; i < kDGWaves; ++i) mx = mred[k & 1][i] > mx ? mred[k & 1][i] : mx;
+      delta = bits_double(mx);
+      if (!(delta > a.eps) || (a.max_iter > 0 && k >= a.max_iter)) break;  // maxent.py:326 / solver.py:40
+    }
+    if (owner) {  // sweep k + 1 of this thread's state (dense_backup's arithmetic and order)
+      double v = SOFT ? ph : 0.0;
+#pragma unroll
+      for (int act = 0; act < AT; ++act) {
+        if (act >= A) break;
+        double dot = red[0][act * RB + tid];
+#pragma unroll
+        for (int w = 1; w < kDGWaves; ++w) dot += red[w][act * RB + tid];
+        if (SOFT) {
+          qkeep[act] = __dadd_rn(rr, __dmul_rn(a.discount, dot));
+          v = softmax2(v, qkeep[act]);  // maxent.py:329-333
+        } else {
+          const double q = __dmul_rn(a.discount, dot);  // solver.py:44
+          if (a.average) v = act == 0 ? q : __dadd_rn(v, q);
+          else v = act == 0 ? q : ((v != v || q <= v) ? v : q);
+        }
+      }
+      if (!SOFT) v = __dadd_rn(rr, a.average ? v / (double)A : v);  // solver.py:47 / :99
+      vkeep = v;
+      const unsigned tag1 = salt | ((unsigned)(k + 1) & 0xFFFFFu);
+      gran_store(rg, ((unsigned)((k + 1) & 1) * (unsigned)S + (unsigned)(row0 + tid)) * 16u, dbits(v), tag1, plain);
+    }
+    ++k;
+    {  // gather v_k and its max |v_k - v_(k-1)| for the next loop test (the forward's ring argument)
+      const unsigned tag = salt | ((unsigned)k & 0xFFFFFu);
+      unsigned off[CPT];
+#pragma unroll
+      for (int j = 0; j < CPT; ++j) off[j] = (unsigned)(k & 1) * 16u * (unsigned)S + off0[j];
+      unsigned long long v[CPT];
+      if (!gran_gather<CPT>(rg, rg, off, want, tag, v)) lflag = 1;
+      unsigned long long d = 0ull;
+#pragma unroll
+      for (int j = 0; j < CPT; ++j) {
+        if (!((want >> j) & 1u)) continue;
+        const double nv = bits_double(v[j]);
+        const unsigned long long dd = abs_bits(nv - cur[j]);
+        d = dd > d ? dd : d;
+        cur[j] = nv;
+      }
+      d = wave_max_u64(d);
+      if (lane == 0) mred[k & 1][wave] = d;
+    }
+  }
+  if (owner) {
+    if (a.value) a.value[srow] = vkeep;
+    if (SOFT)
+      for (int act = 0; act < A; ++act) a.out[srow * A + act] = exp(qkeep[act] - vkeep);  // maxent.py:341
+  }
+  if (blk == 0 && tid == 0) {
+    if (a.iters) a.iters[b] = k;
+    a.status[b] = dg_finish_status(delta, a.eps);
+  }
+}
+
 // ---------------------------------------------------------------------------
 // host side
 // ---------------------------------------------------------------------------
@@ -418,6 +620,20 @@ int capacity(void* fn) {
 
 std::atomic<unsigned> g_dg_salt{1};
 
+// (AT, RB, CPT) instantiations of the Bellman kernel: AT * RB a multiple of 16,
+// AT * RB * CPT <= 64 doubles, and at most 256 workgroups per instance
+template <bool SOFT>
+void* dense_bellman_grid_fn_s(int at, int rb, int cpt) {
+#define IRLMX_DBG(T, R, C) \
+  if (at == T && rb == R && cpt == C) return (void*)&dense_bellman_grid_kernel<SOFT, T, R, C>;
+  IRLMX_DBG(4, 4, 1) IRLMX_DBG(4, 4, 2) IRLMX_DBG(4, 8, 1) IRLMX_DBG(4, 8, 2) IRLMX_DBG(4, 16, 1)
+  IRLMX_DBG(8, 2, 1) IRLMX_DBG(8, 4, 1) IRLMX_DBG(8, 4, 2) IRLMX_DBG(8, 8, 1)
+#undef IRLMX_DBG
+  return nullptr;
+}
+
+int bellman_at(int A) { return A <= 4 ? 4 : (A <= 8 ? 8 : 0); }
+
 }  // namespace
 
 bool dense_grid_plan(int mode, int S, int B, DenseGridPlan* out) {
@@ -454,15 +670,48 @@ bool dense_grid_plan(int mode, int S, int B, DenseGridPlan* out) {
       if ((long long)bpi * B > cap) continue;
       const bool fits = cap >= 8 && bpi <= kDG && (long long)((B + 7) / 8) * bpi <= cus / 8;
       if (pass == 0 && !fits) continue;
-      *out = DenseGridPlan{rb, cpt, bpi, pass == 0 ? 1 : 0};
+      *out = DenseGridPlan{rb, cpt, bpi, pass == 0 ? 1 : 0, 0};
       return true;
     }
   }
   return false;
 }
 
-int dense_grid_run(int mode, const DenseGridPlan& p, DenseGridArgs a, hipStream_t st) {
-  a.rb = p.rb;
+// Soft VI / VI: the fewest rows per workgroup that fit (a row costs A dots and
+// the fold), XCD-grouped when one XCD holds each group of 8 instances.
+bool dense_bellman_grid_plan(int S, int B, int A, DenseGridPlan* out) {
+  if (env_int("IRLMX_DENSE_GRID", 1) == 0 || S <= 0 || B <= 0) return false;
+  const int at = bellman_at(A);
+  const int cpt = S <= kDG ? 1 : (S <= 2 * kDG ? 2 : 0);
+  if (!at || !cpt) return false;
+  const int forced = env_int("IRLMX_DENSE_GRID_RB", 0);
+  const int f_cus = env_int("IRLMX_PLAN_CUS", 0);
+  const int cus = f_cus > 0 ? f_cus : device_cus();
+  if (cus <= 0) return false;
+  const int fx = env_int("IRLMX_DENSE_GRID_XCD", -1);
+  const bool xcd_ok = env_int("IRLMX_XCD_GROUP", 1) != 0 && fx != 0;
+  for (int pass = 0; pass < 2; ++pass) {
+    if (pass == 0 && !xcd_ok) continue;
+    if (pass > 0 && fx == 1) break;
+    for (int rb = 2; rb <= 16; rb *= 2) {
+      if (forced > 0 && rb != forced) continue;
+      void* fn = dense_bellman_grid_fn_s<true>(at, rb, cpt);
+      if (!fn) continue;
+      const int bpi = (S + rb - 1) / rb;
+      if ((long long)bpi * B > cus) continue;
+      const int cap = std::min(capacity(fn), capacity(dense_bellman_grid_fn_s<false>(at, rb, cpt)));
+      if ((long long)bpi * B > cap) continue;
+      const bool fits = cap >= 8 && bpi <= kDG && (long long)((B + 7) / 8) * bpi <= cus / 8;
+      if (pass == 0 && !fits) continue;
+      *out = DenseGridPlan{rb, cpt, bpi, pass == 0 ? 1 : 0, at};
+      return true;
+    }
+  }
+  return false;
+}
+
+static int launch_grid(void* fn, const DenseGridPlan& p, DenseGridArgs a, int rows, hipStream_t st) {
+  a.rb = rows;
   a.bpi = p.bpi;
   a.nb = a.B;
   a.xcd_group = p.xcd;
@@ -471,7 +720,7 @@ int dense_grid_run(int mode, const DenseGridPlan& p, DenseGridArgs a, hipStream_
   a.n_resident = p.bpi * a.B + (env_int("IRLMX_TEST_NOT_RESIDENT", 0) ? 1 : 0);
   const int grid = p.xcd ? 8 * ((a.B + 7) / 8) * p.bpi : p.bpi * a.B;
   void* args[] = {&a};
-  hipError_t e = hipLaunchKernel(dense_grid_fn(mode, p.rb, p.cpt), dim3(grid), dim3(kDG), args, 0, st);
+  hipError_t e = hipLaunchKernel(fn, dim3(grid), dim3(kDG), args, 0, st);
   if (e != hipSuccess) return hip_fail(e, "dense grid launch");
   count_event(IRLMX_CTR_GRID_LAUNCHES);
   int err = 0;
@@ -489,6 +738,20 @@ int dense_grid_run(int mode, const DenseGridPlan& p, DenseGridArgs a, hipStream_
     return e == hipSuccess ? kClusterNotResident : hip_fail(e, "dense grid err reset");
   }
   return 0;
+}
+
+int dense_bellman_grid_run(bool soft, const DenseGridPlan& p, DenseGridArgs a, hipStream_t st) {
+  const int at = p.at, rb = p.rb;
+  void* fn = soft ? dense_bellman_grid_fn_s<true>(at, rb, p.cpt) : dense_bellman_grid_fn_s<false>(at, rb, p.cpt);
+  if (!fn) {
+    set_error("dense bellman grid: no kernel for %d actions, %d rows, %d columns per thread", at, rb, p.cpt);
+    return IRLMX_EINVAL;
+  }
+  return launch_grid(fn, p, a, rb, st);
+}
+
+int dense_grid_run(int mode, const DenseGridPlan& p, DenseGridArgs a, hipStream_t st) {
+  return launch_grid(dense_grid_fn(mode, p.rb, p.cpt), p, a, p.rb, st);
 }
 
 }  // namespace irlmx

@@ -1593,8 +1593,10 @@ static bool dense_gemm(const Model& m) {
 // whenever the rows fit in registers at one workgroup per CU (dense_grid.hip);
 // a backward that the planner gives to the GEMM keeps it.
 static bool dense_grid(const Model& m, int op, DenseGridPlan* out) {
-  if (!m.dense || (op != IRLMX_OP_FORWARD && op != IRLMX_OP_BACKWARD)) return false;
-  if (op == IRLMX_OP_BACKWARD && dense_gemm(m)) return false;
+  if (!m.dense) return false;
+  if (op != IRLMX_OP_FORWARD && dense_gemm(m)) return false;
+  if (op == IRLMX_OP_SOFT_BACKWARD || op == IRLMX_OP_VALUE_ITERATION) return dense_bellman_grid_plan(m.S, m.B, m.A, out);
+  if (op != IRLMX_OP_FORWARD && op != IRLMX_OP_BACKWARD) return false;
   return dense_grid_plan(op == IRLMX_OP_FORWARD ? kModeFwd : kModeBwd, m.S, m.B, out);
 }
 
@@ -1708,6 +1710,7 @@ extern "C" int irlmx_execution_plan(const irlmx_mdp* mdp, int32_t op, int64_t* p
     plan[3] = dp.bpi;
     plan[4] = m.B;
     plan[5] = dp.cpt;   // columns per thread
+    plan[6] = dp.at;    // soft VI / VI: actions compiled per state (0: forward / backward)
     plan[7] = kDenseGridThreads;
     plan[8] = 1;
     return 0;
@@ -1917,6 +1920,15 @@ static int bellman_common(const irlmx_mdp* mdp, const double* reward, const doub
     const DenseBellman db{reward, phi, discount, eps, (long long)max_iter, average, soft ? 1 : 0, p_action, value,
                           iterations, status};
     const bool gemm = dense_gemm(m);  // the P . [v_1 .. v_B] products on the MFMA kernel
+    DenseGridPlan dp;
+    if (dense_grid(m, op, &dp)) {  // one persistent launch, the A rows of each state in registers
+      DenseGridArgs ga = dense_grid_args(m, ws);
+      ga.P = m.row_val; ga.vin = reward; ga.phi = phi; ga.discount = discount; ga.average = average;
+      ga.value = value; ga.eps = eps; ga.max_iter = (long long)max_iter;
+      ga.out = p_action; ga.iters = iterations; ga.status = status;
+      const int rc = dense_bellman_grid_run(soft, dp, ga, st);
+      if (rc != kClusterNotResident) return rc;  // else: the per-sweep shape below
+    }
     hipError_t gerr = hipSuccess;
     int rc = run_until_done(ws, m.B, st, [&](long long it, int r3) {
       if (gemm) {

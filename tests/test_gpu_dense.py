@@ -73,9 +73,9 @@ def test_generic_fixtures_on_dense_layout(dev):
         P = z[c + "__P"]
         mdp = DeviceMDP.from_dense(P, device=dev, layout="dense")
         assert mdp.layout == _lib.LAYOUT_DENSE
-        # forward / backward: the persistent dense shape (test_gpu_dense_grid.py); soft VI / VI per sweep
+        # every pass on the persistent dense shape (test_gpu_dense_grid.py)
         assert ops.execution_plan(mdp, "forward")["shape"] == "dense-grid"
-        assert ops.execution_plan(mdp, "soft_backward")["shape"] == "dense"
+        assert ops.execution_plan(mdp, "soft_backward")["shape"] == "dense-grid"
         term = [int(t) for t in z[c + "__terminal"]]
         got = run_all(mdp, z[c + "__reward"], term, z[c + "__p0"], dev)
         close(got["pi"], z[c + "__pi"], 1e-9, c + " pi")

@@ -1,8 +1,9 @@
 """Persistent dense shape (IRLMX_SHAPE_DENSE_GRID, csrc/dense_grid.hip).
 
-The forward (maxent.py:98-112) and the collapsed backward (maxent.py:143-159)
-of DENSE models in one launch per call, each workgroup holding its rows of the
-S x S matrix in registers and the swept vector exchanged as tagged granules.
+The forward (maxent.py:98-112), the collapsed backward (maxent.py:143-159) and
+soft VI / VI (maxent.py:326-341, solver.py:40-50 / 95-100) of DENSE models in
+one launch per call, each workgroup holding its rows of the S x S matrices in
+registers and the swept vector exchanged as tagged granules.
 Checked against the per-sweep dense kernels (IRLMX_DENSE_GRID=0: one launch per
 sweep, csrc/dense.hip) and the dense oracle: sweep counts and statuses
 identical, values within 1e-12 relative (only the summation order of each row
@@ -238,3 +239,70 @@ def test_dense_grid_not_resident_rerun(dev, monkeypatch):
     after = ops.counters()
     assert after["rerun_not_resident"] == before["rerun_not_resident"] + 1
     assert torch.equal(got, ref)
+
+
+BELLMAN_CASES = [  # S, A, B, shared
+    (7, 3, 1, True), (64, 4, 2, False), (300, 4, 3, True), (513, 4, 2, True), (1000, 4, 1, True),
+    (200, 5, 2, True), (700, 6, 1, True), (130, 8, 3, False),
+]
+
+
+@pytest.mark.parametrize("n,A,batch,shared", BELLMAN_CASES)
+def test_dense_grid_soft_vi_and_vi(dev, monkeypatch, n, A, batch, shared):
+    """Soft VI (discount 0.7; pi and value) and VI (max and mean over actions) on
+    the dense grid shape against the per-sweep dense kernels: sweep counts and
+    statuses identical, values and policies within 1e-12; and against the dense
+    oracle for the first instance."""
+    from irlmx import ops
+    from irlmx.batch import terminal_reward
+    mdp, Ps = dense_model(dev, n, A, batch, shared, seed=3 * n + A)
+    for op in ("soft_backward", "value_iteration"):
+        plan = ops.execution_plan(mdp, op)
+        assert plan["shape"] == "dense-grid" and plan["layout"] == (4 if A <= 4 else 8), (op, plan)
+    r = np.random.default_rng(n).uniform(0.0, 1.0, (batch, n))
+    phi = terminal_reward([n - 1], n, batch, dev)
+
+    def run():
+        pi, v, k, st = ops.soft_backward(mdp, r, phi, 0.7)
+        vi, kv, stv = ops.value_iteration(mdp, r, 0.9)
+        va, kva, sta = ops.value_iteration(mdp, r, 0.9, average=True)
+        return [x.cpu().numpy() for x in (pi, v, k, st, vi, kv, stv, va, kva, sta)]
+
+    g, sw = both_shapes(monkeypatch, run)
+    for i in (2, 3, 5, 6, 8, 9):  # sweep counts and statuses
+        assert np.array_equal(g[i], sw[i]), (i, g[i], sw[i])
+    for i in (0, 1, 4, 7):
+        assert rel(g[i], sw[i]) <= RTOL, i
+    pi_ref, v_ref, k_ref = O.soft_backward(Ps[0], [n - 1], r[0], 0.7)
+    assert int(g[2][0]) == k_ref
+    assert rel(g[0][0], pi_ref) <= 1e-9 and rel(g[1][0], v_ref) <= 1e-9
+    vv_ref, kv_ref = O.value_iteration(Ps[0], r[0], 0.9)
+    assert int(g[5][0]) == kv_ref and rel(g[4][0], vv_ref) <= 1e-9
+
+
+@pytest.mark.parametrize("n,A,rb", [(300, 4, 4), (300, 4, 8), (300, 4, 16), (900, 4, 4), (900, 4, 8),
+                                    (200, 7, 2), (200, 7, 4), (200, 7, 8), (800, 7, 4)])
+def test_dense_bellman_grid_every_instantiation(dev, monkeypatch, n, A, rb):
+    """Every (actions compiled, rows, columns per thread) instantiation of the
+    Bellman kernel, forced by IRLMX_DENSE_GRID_RB (spread over the chip), with a
+    sweep cap: soft VI and VI against the per-sweep dense kernels."""
+    from irlmx import ops
+    from irlmx.batch import terminal_reward
+    mdp, _ = dense_model(dev, n, A, 1, True, seed=n + rb)
+    monkeypatch.setenv("IRLMX_DENSE_GRID_RB", str(rb))
+    monkeypatch.setenv("IRLMX_DENSE_GRID_XCD", "0")
+    plan = ops.execution_plan(mdp, "soft_backward")
+    assert plan["shape"] == "dense-grid" and plan["R"] == rb and plan["G"] == 0, plan
+    r = np.random.default_rng(rb).uniform(0.0, 1.0, (1, n))
+    phi = terminal_reward([n - 1], n, 1, dev)
+
+    def run():
+        pi, v, k, st = ops.soft_backward(mdp, r, phi, 0.7, max_iter=40)
+        vi, kv, stv = ops.value_iteration(mdp, r, 0.9)
+        return [x.cpu().numpy() for x in (pi, v, k, st, vi, kv, stv)]
+
+    g, sw = both_shapes(monkeypatch, run)
+    assert int(g[2][0]) == int(sw[2][0]) and int(g[3][0]) == int(sw[3][0])
+    assert np.array_equal(g[5], sw[5]) and np.array_equal(g[6], sw[6])
+    for i in (0, 1, 4):
+        assert rel(g[i], sw[i]) <= RTOL, i

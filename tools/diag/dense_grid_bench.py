@@ -8,6 +8,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)
 sys.path[:0] = [os.path.join(ROOT, "irl-maxent_amd")]
 import numpy as np, torch
 from irlmx import DeviceMDP, ops
+from irlmx.batch import terminal_reward
 
 dev = torch.device("cuda", 0)
 
@@ -47,8 +48,14 @@ for S in sizes:
             tb, _ = timed(lambda: ops.backward_maxent(mdp, r, tm))
             tf, (svf, k, _) = timed(lambda: ops.forward_svf(mdp, p0, tm, pi, max_iter=4000))
             kk = int(k.max())
+            phi = terminal_reward([S - 1], S, B, dev)
+            ps = ops.execution_plan(mdp, "soft_backward")
+            tsv, (_, _, ks, _) = timed(lambda: ops.soft_backward(mdp, r, phi, 0.7))
+            tvi, (_, kv, _) = timed(lambda: ops.value_iteration(mdp, r, 0.9))
             print(f"S={S} B={B} {name:13s} [{plan['shape']} R={plan['R']} C={plan['C']} cpt={plan['spt']} xcd={plan['G']}]: "
                   f"backward {tb * 1e3:.2f} ms = {tb / (2 * S) * 1e6:.2f} us/sweep; forward {kk} sweeps "
-                  f"{tf * 1e3:.2f} ms = {tf / kk * 1e6:.2f} us/sweep", flush=True)
+                  f"{tf * 1e3:.2f} ms = {tf / kk * 1e6:.2f} us/sweep; [{ps['shape']} R={ps['R']} xcd={ps['G']}] "
+                  f"soft VI {int(ks.max())} sweeps {tsv / int(ks.max()) * 1e6:.2f} us/sweep; "
+                  f"VI {int(kv.max())} sweeps {tvi / int(kv.max()) * 1e6:.2f} us/sweep", flush=True)
         for k in ("IRLMX_DENSE_GRID", "IRLMX_DENSE_GRID_RB", "IRLMX_DENSE_GRID_XCD"):
             os.environ.pop(k, None)

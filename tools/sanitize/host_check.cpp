@@ -120,11 +120,14 @@ static void check_plan(const irlmx_mdp& m, int op, const int64_t* p, const char*
   } else if (shape == IRLMX_SHAPE_DENSE || shape == IRLMX_SHAPE_DENSE_GEMM) {
     CHECK(m.layout == IRLMX_LAYOUT_DENSE, "%s: dense shape for layout %d", what, m.layout);
   } else if (shape == IRLMX_SHAPE_DENSE_GRID) {
-    const int64_t rb = p[1], bpi = p[3], cpt = p[5];
-    CHECK(m.layout == IRLMX_LAYOUT_DENSE && (op == IRLMX_OP_BACKWARD || op == IRLMX_OP_FORWARD), "%s", what);
+    const int64_t rb = p[1], bpi = p[3], cpt = p[5], at = p[6];
+    const bool bellman = op == IRLMX_OP_SOFT_BACKWARD || op == IRLMX_OP_VALUE_ITERATION;
+    CHECK(m.layout == IRLMX_LAYOUT_DENSE, "%s", what);
     CHECK(p[7] == 512 && p[4] == m.batch && p[8] == 1, "%s: dense grid threads %lld", what, (long long)p[7]);
-    CHECK(rb >= 4 && rb <= 64 && rb * cpt <= 64, "%s: dense grid rb %lld cpt %lld", what, (long long)rb,
-          (long long)cpt);
+    CHECK(bellman ? (at >= m.n_actions && (at == 4 || at == 8)) : at == 0, "%s: dense grid actions %lld", what,
+          (long long)at);
+    CHECK(rb >= (bellman ? 2 : 4) && rb <= 64 && rb * cpt * (bellman ? at : 1) <= 64,
+          "%s: dense grid rb %lld cpt %lld", what, (long long)rb, (long long)cpt);
     CHECK(cpt * 512 >= m.n_states && bpi == (m.n_states + rb - 1) / rb, "%s: dense grid covers", what);
     CHECK(bpi * m.batch <= kCus, "%s: dense grid %lld x %d workgroups", what, (long long)bpi, m.batch);
   }
