@@ -182,9 +182,10 @@ int irlmx_value_iteration(const irlmx_mdp* mdp, const double* reward, double dis
 #define IRLMX_SHAPE_DENSE_GEMM 4 /* DENSE, shared table: the backward sweep as one dgemm over all instances */
 #define IRLMX_SHAPE_GRID 5    /* soft VI / VI on large grids: one persistent launch, values exchanged per sweep
                                  ([3] = workgroups per instance) */
-#define IRLMX_SHAPE_DENSE_GRID 6 /* DENSE forward / backward: one persistent launch, [1] matrix rows per
-                                    workgroup held in registers, [5] columns per thread, [3] workgroups per
-                                    instance, values exchanged per sweep */
+#define IRLMX_SHAPE_DENSE_GRID 6 /* DENSE forward / backward / soft VI / VI: one persistent launch, [1] states
+                                    per workgroup whose matrix rows sit in registers, [5] columns per thread,
+                                    [3] workgroups per instance, [2] 1 = each instance on one XCD, [6] soft VI /
+                                    VI: actions compiled per state; values exchanged per sweep */
 #define IRLMX_PLAN_NO_RESCALE 0x100 /* OR into op (IRLMX_OP_BACKWARD only): the plan of a rescale = 0 call, which
                                       never takes the cluster shape (its overflow bookkeeping is per sweep) */
 int irlmx_execution_plan(const irlmx_mdp* mdp, int32_t op, int64_t* plan);
