@@ -105,7 +105,7 @@ const char* irlmx_last_error(void);
  */
 #define IRLMX_COUNTERS_LEN 6
 #define IRLMX_CTR_CLUSTER_LAUNCHES 0   /* persistent cluster launches (stencil forward / backward) */
-#define IRLMX_CTR_GRID_LAUNCHES 1      /* persistent grid launches (soft VI / VI / ELL passes) */
+#define IRLMX_CTR_GRID_LAUNCHES 1      /* persistent grid and dense grid launches (soft VI / VI, ELL and DENSE passes) */
 #define IRLMX_CTR_RERUN_NONFINITE 2    /* cluster forward saw a non-finite value: rerun per sweep (exact NaN rules) */
 #define IRLMX_CTR_RERUN_NOT_RESIDENT 3 /* workgroups could not all run at once: rerun per sweep */
 #define IRLMX_CTR_RERUN_TIMEOUT 4      /* a halo / value exchange timed out (a descheduled workgroup): rerun per sweep */
