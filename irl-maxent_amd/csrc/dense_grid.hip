@@ -678,7 +678,9 @@ bool dense_grid_plan(int mode, int S, int B, DenseGridPlan* out) {
 }
 
 // Soft VI / VI: the fewest rows per workgroup that fit (a row costs A dots and
-// the fold), XCD-grouped when one XCD holds each group of 8 instances.
+// the fold); XCD-grouped only at <= 8 rows per workgroup (measured,
+// profiles/r03_dense_bellman_grid_variants.txt: S = 256 one XCD at 8 rows 3.2 us
+// per sweep vs 3.5 spread; S = 512 one XCD needs 16 rows, 4.3 vs 3.9 spread at 4).
 bool dense_bellman_grid_plan(int S, int B, int A, DenseGridPlan* out) {
   if (env_int("IRLMX_DENSE_GRID", 1) == 0 || S <= 0 || B <= 0) return false;
   const int at = bellman_at(A);
@@ -701,7 +703,7 @@ bool dense_bellman_grid_plan(int S, int B, int A, DenseGridPlan* out) {
       if ((long long)bpi * B > cus) continue;
       const int cap = std::min(capacity(fn), capacity(dense_bellman_grid_fn_s<false>(at, rb, cpt)));
       if ((long long)bpi * B > cap) continue;
-      const bool fits = cap >= 8 && bpi <= kDG && (long long)((B + 7) / 8) * bpi <= cus / 8;
+      const bool fits = cap >= 8 && bpi <= kDG && (long long)((B + 7) / 8) * bpi <= cus / 8 && (rb <= 8 || fx == 1);
       if (pass == 0 && !fits) continue;
       *out = DenseGridPlan{rb, cpt, bpi, pass == 0 ? 1 : 0, at};
       return true;

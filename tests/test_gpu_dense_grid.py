@@ -172,6 +172,20 @@ def test_dense_grid_planner(dev, n, batch, plan):
         assert (p["shape"], p["R"], p["C"], p["G"]) == ("dense-grid",) + plan, (op, p)
 
 
+@pytest.mark.parametrize("n,A,batch,plan", [(256, 4, 1, (8, 32, 1, 4)), (512, 4, 1, (4, 128, 0, 4)),
+                                            (1024, 4, 1, (4, 256, 0, 4)), (256, 6, 2, (8, 32, 1, 8))])
+def test_dense_bellman_grid_planner(dev, n, A, batch, plan):
+    """Soft VI / VI plans: one XCD per instance group only at <= 8
+    states per workgroup, else the fewest states per workgroup spread over the
+    chip; (states per workgroup, workgroups per instance, XCD-grouped, actions
+    compiled)."""
+    from irlmx import ops
+    mdp, _ = dense_model(dev, n, A, batch, True, seed=2)
+    for op in ("soft_backward", "value_iteration"):
+        p = ops.execution_plan(mdp, op)
+        assert (p["shape"], p["R"], p["C"], p["G"], p["layout"]) == ("dense-grid",) + plan, (op, p)
+
+
 def test_dense_grid_loop_edges(dev, monkeypatch):
     """The loop rules at their edges, dense grid vs per-sweep dense shape: a
     max_iter cap (status MAXITER, values after exactly 5 sweeps), a non-finite
