@@ -22,6 +22,7 @@
 #include <hip/hip_runtime.h>
 
 #include <atomic>
+#include <cstdlib>
 
 #include "dense.h"
 
@@ -441,6 +442,10 @@ dense_bellman_finish_kernel(DenseView d, DenseBellman a, DenseBufs w) {
 // rows start 16-byte aligned only when S is even (V2: two 16-byte loads per
 // operand row and chunk), else the kernel loads doubles one by one.
 typedef double f64x4 __attribute__((ext_vector_type(4)));
+#ifndef IRLMX_GEMM_PF
+#define IRLMX_GEMM_PF 1
+#endif
+constexpr int kGemmPrefetch = IRLMX_GEMM_PF;  // K chunks whose loads are in flight during a chunk's MFMAs
 
 // ST 16-row tiles of M and NBT 16-instance column tiles per workgroup (sized to
 // S and B so that the grid fills the chip)
@@ -503,21 +508,39 @@ dense_gemm_kernel(const double* __restrict__ M, const double* __restrict__ Z, do
     for (int bt = 0; bt < NBT; ++bt) load4(zrow[bt], t, tok && zok[bt], zo[bt]);
   };
   auto el = [](const double2 (&v)[2], int x) { return x == 0 ? v[0].x : x == 1 ? v[0].y : x == 2 ? v[1].x : v[1].y; };
-  load(c0, ma, za);
-  for (int c = c0; c < c1; ++c) {
-    double2 mn[ST][2], zn[NBT][2];
-    load(c + 1, mn, zn);  // next chunk in flight during this chunk's MFMAs
+  auto mfmas = [&](const double2 (&mo)[ST][2], const double2 (&zo)[NBT][2]) {
 #pragma unroll
     for (int x = 0; x < 4; ++x)
 #pragma unroll
       for (int st = 0; st < ST; ++st)
 #pragma unroll
         for (int bt = 0; bt < NBT; ++bt)
-          acc[st][bt] = __builtin_amdgcn_mfma_f64_16x16x4f64(el(ma[st], x), el(za[bt], x), acc[st][bt], 0, 0, 0);
+          acc[st][bt] = __builtin_amdgcn_mfma_f64_16x16x4f64(el(mo[st], x), el(zo[bt], x), acc[st][bt], 0, 0, 0);
+  };
+  if constexpr (kGemmPrefetch <= 1) {
+    load(c0, ma, za);
+    for (int c = c0; c < c1; ++c) {
+      double2 mn[ST][2], zn[NBT][2];
+      load(c + 1, mn, zn);  // next chunk in flight during this chunk's MFMAs
+      mfmas(ma, za);
 #pragma unroll
-    for (int st = 0; st < ST; ++st) { ma[st][0] = mn[st][0]; ma[st][1] = mn[st][1]; }
+      for (int st = 0; st < ST; ++st) { ma[st][0] = mn[st][0]; ma[st][1] = mn[st][1]; }
 #pragma unroll
-    for (int bt = 0; bt < NBT; ++bt) { za[bt][0] = zn[bt][0]; za[bt][1] = zn[bt][1]; }
+      for (int bt = 0; bt < NBT; ++bt) { za[bt][0] = zn[bt][0]; za[bt][1] = zn[bt][1]; }
+    }
+  } else {
+    // a ring of kGemmPrefetch + 1 chunk buffers: kGemmPrefetch chunks in flight
+    constexpr int PF = kGemmPrefetch, NR = kGemmPrefetch + 1;
+    double2 mr[NR][ST][2], zr[NR][NBT][2];
+#pragma unroll
+    for (int p = 0; p < PF; ++p) load(c0 + p, mr[p], zr[p]);
+    for (int c = c0; c < c1; c += NR) {
+#pragma unroll
+      for (int u = 0; u < NR; ++u) {
+        load(c + u + PF, mr[(u + PF) % NR], zr[(u + PF) % NR]);
+        if (c + u < c1) mfmas(mr[u], zr[u]);
+      }
+    }
   }
   // split-K partials -> LDS, summed in wave order
 #pragma unroll
@@ -678,28 +701,50 @@ static hipError_t gemm_waves(const double* M, const double* Z, double* C, int R,
   return gemm_go<ST, NBT, 8>(M, Z, C, R, S, B, st);
 }
 
-hipError_t dense_gemm_launch(const double* M, const double* Z, double* C, int R, int S, int B, hipStream_t st) {
-  const int nbt = B <= 16 ? 1 : (B <= 32 ? 2 : 4);
-  const int ny = (B + 16 * nbt - 1) / (16 * nbt);
-  // two row tiles per wave (half the Z re-reads) while that still gives >= 256 workgroups
-  const bool st2 = (long long)((R + 31) / 32) * ny >= 256;
-  if (st2) {
-    if (nbt == 1) return gemm_waves<2, 1>(M, Z, C, R, S, B, st);
-    if (nbt == 2) return gemm_waves<2, 2>(M, Z, C, R, S, B, st);
-    return gemm_waves<2, 4>(M, Z, C, R, S, B, st);
+// Tiles per workgroup (ST row tiles x NBT instance tiles of 16): the largest,
+// squarest workgroup tile that still gives >= 256 workgroups (one per CU) --
+// a workgroup reads 16 (ST + NBT) rows of M and Z per K chunk for 256 ST NBT
+// outputs, so a 32 x 32 tile moves the least (S = 4096, B = 64: 2 x 2 tiles
+// 69 us vs 1 x 4 81 us; S = 2048, B = 64: 2 x 1 26 us vs 1 x 4 on half the CUs
+// 41 us, profiles/r03_dense_gemm_tiles.txt); else the most workgroups (1 x 1).
+// IRLMX_GEMM_NBT forces the instance tiles (diagnostics).
+static void gemm_tiles(int R, int B, int* st, int* nbt) {
+  const int rt = (R + 15) / 16, ct = (B + 15) / 16;
+  const char* f = getenv("IRLMX_GEMM_NBT");
+  const int forced = (f && (*f == '1' || *f == '2' || *f == '4') && f[1] == 0) ? *f - '0' : 0;
+  static const int cands[][2] = {{2, 4}, {2, 2}, {1, 4}, {2, 1}, {1, 2}, {1, 1}};
+  for (const auto& c : cands) {
+    if (forced ? c[1] != forced : (c[1] > ct || c[0] > rt)) continue;
+    if ((long long)((rt + c[0] - 1) / c[0]) * ((ct + c[1] - 1) / c[1]) >= 256 || (c[0] == 1 && (forced || c[1] == 1))) {
+      *st = c[0];
+      *nbt = c[1];
+      return;
+    }
   }
-  if (nbt == 1) return gemm_waves<1, 1>(M, Z, C, R, S, B, st);
-  if (nbt == 2) return gemm_waves<1, 2>(M, Z, C, R, S, B, st);
-  return gemm_waves<1, 4>(M, Z, C, R, S, B, st);
+  *st = 1;
+  *nbt = forced ? forced : 1;
+}
+
+template <int ST>
+static hipError_t gemm_nbt_go(int nbt, const double* M, const double* Z, double* C, int R, int S, int B,
+                              hipStream_t st) {
+  if (nbt == 1) return gemm_waves<ST, 1>(M, Z, C, R, S, B, st);
+  if (nbt == 2) return gemm_waves<ST, 2>(M, Z, C, R, S, B, st);
+  return gemm_waves<ST, 4>(M, Z, C, R, S, B, st);
+}
+
+hipError_t dense_gemm_launch(const double* M, const double* Z, double* C, int R, int S, int B, hipStream_t st) {
+  int ts = 1, nbt = 1;
+  gemm_tiles(R, B, &ts, &nbt);
+  return ts == 2 ? gemm_nbt_go<2>(nbt, M, Z, C, R, S, B, st) : gemm_nbt_go<1>(nbt, M, Z, C, R, S, B, st);
 }
 
 // the kernel variant a launch of these sizes runs: {ST, NBT, waves, V2}
 void dense_gemm_variant(int R, int S, int B, int* out) {
-  const int nbt = B <= 16 ? 1 : (B <= 32 ? 2 : 4);
-  const int ny = (B + 16 * nbt - 1) / (16 * nbt);
-  const int st = (long long)((R + 31) / 32) * ny >= 256 ? 2 : 1;
-  const long long wgs = (long long)((R + 16 * st - 1) / (16 * st)) * ny;
-  out[0] = st;
+  int ts = 1, nbt = 1;
+  gemm_tiles(R, B, &ts, &nbt);
+  const long long wgs = (long long)((R + 16 * ts - 1) / (16 * ts)) * ((B + 16 * nbt - 1) / (16 * nbt));
+  out[0] = ts;
   out[1] = nbt;
   out[2] = wgs >= 512 ? 4 : 8;
   out[3] = S % 2 == 0 ? 1 : 0;
