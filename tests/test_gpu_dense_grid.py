@@ -237,7 +237,8 @@ def test_dense_grid_loop_edges(dev, monkeypatch):
 def test_dense_grid_not_resident_rerun(dev, monkeypatch):
     """A launch whose workgroups cannot all run at once (IRLMX_TEST_NOT_RESIDENT:
     the rendezvous waits for one workgroup more than launched) reruns the call on
-    the per-sweep dense shape, with its results, and counts the rerun."""
+    the per-sweep dense shape, with its results, and counts the rerun (backward
+    and soft VI)."""
     from irlmx import ops
     n = 400
     mdp, _ = dense_model(dev, n, 4, 2, True, seed=11)
@@ -253,6 +254,20 @@ def test_dense_grid_not_resident_rerun(dev, monkeypatch):
     after = ops.counters()
     assert after["rerun_not_resident"] == before["rerun_not_resident"] + 1
     assert torch.equal(got, ref)
+    # soft VI likewise
+    from irlmx.batch import terminal_reward
+    phi = terminal_reward([n - 1], n, 2, dev)
+    monkeypatch.setenv("IRLMX_DENSE_GRID", "0")
+    ref = ops.soft_backward(mdp, r, phi, 0.7)
+    monkeypatch.delenv("IRLMX_DENSE_GRID")
+    assert ops.execution_plan(mdp, "soft_backward")["shape"] == "dense-grid"
+    before = ops.counters()
+    monkeypatch.setenv("IRLMX_TEST_NOT_RESIDENT", "1")
+    got = ops.soft_backward(mdp, r, phi, 0.7)
+    monkeypatch.delenv("IRLMX_TEST_NOT_RESIDENT")
+    assert ops.counters()["rerun_not_resident"] == before["rerun_not_resident"] + 1
+    for x, y in zip(got, ref):
+        assert torch.equal(x, y)
 
 
 BELLMAN_CASES = [  # S, A, B, shared
