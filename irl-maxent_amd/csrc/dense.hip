@@ -13,11 +13,14 @@
 //   VI         v'[s] = r[s] + max_a / mean_a g (P_a v)[s]            (solver.py:40-50, 95-100)
 //
 // All are HBM-stream bound (S^2 doubles per sweep per table and instance).
-// With one table shared by B instances the backward sweep is a GEMM
-// (M . [zs_1 .. zs_B]); fixed_point.hip then runs it as a library dgemm plus the
-// epilogue below, or streams M once per instance -- whichever the planner's
-// measured crossover picks.  Convergence bookkeeping follows the
-// sweep shape of fixed_point.hip (3-slot max ring, done flags, host polling).
+// With one table shared by B instances the sweep is a GEMM (M . [zs_1 .. zs_B],
+// or the stacked P_a for soft VI / VI); fixed_point.hip then runs it on the
+// hand-written fp64 MFMA kernel below plus an epilogue, or streams M once per
+// instance -- whichever the planner's measured crossover picks (dense_gemm()
+// in fixed_point.hip: from 16 instances, from 4 at S >= 4096).  Up to S = 2048
+// the persistent dense shape (dense_grid.hip) takes the calls the GEMM does not.
+// Convergence bookkeeping follows the sweep shape of fixed_point.hip (3-slot
+// max ring, done flags, host polling).
 
 #include <hip/hip_runtime.h>
 
