@@ -1,4 +1,4 @@
-"""Multi-process paths of the instance sharding (gloo, world size 2).
+"""Multi-process paths of the instance sharding (gloo, world sizes 2 and 4).
 
 CPU: shard ranges cover every instance exactly once; the timing max-reduction
 and the result gather work over gloo.  GPU: two ranks share cuda:0 and each
@@ -88,10 +88,10 @@ BENCH_WORKER = textwrap.dedent("""
     import json, os, sys, time
     sys.path[:0] = [{root!r}, {pkg!r}]
     import torch.distributed as dist
-    dist.init_process_group("gloo", init_method="tcp://127.0.0.1:{port}", rank={rank}, world_size=2)
+    dist.init_process_group("gloo", init_method="tcp://127.0.0.1:{port}", rank={rank}, world_size={world})
     import bench
     from irlmx.shard import instance_slips, max_over_ranks, shard_range
-    rank, world, per_gpu = dist.get_rank(), 2, 4
+    rank, world, per_gpu = dist.get_rank(), {world}, 4
     lo, hi = shard_range(per_gpu * world, world, rank)
     done = []
     def step(i, timed):  # stub: rank 1 is the slow rank
@@ -107,26 +107,28 @@ BENCH_WORKER = textwrap.dedent("""
 """)
 
 
-def test_bench_timing_over_gloo(tmp_path):
-    """bench.py's multi-rank arithmetic with a stubbed step (gloo, 2 ranks): each
-    rank times exactly K steps after W warm-ups between barriers, the elapsed time
-    is the max over ranks, value = instances on all ranks x K / that max, and the
-    shards cover the global batch with the bench's per-instance slips."""
+@pytest.mark.parametrize("world", [2, 4])
+def test_bench_timing_over_gloo(tmp_path, world):
+    """bench.py's multi-rank arithmetic with a stubbed step (gloo, 2 and 4 ranks):
+    each rank times exactly K steps after W warm-ups between barriers, the elapsed
+    time is the max over ranks, value = instances on all ranks x K / that max, and
+    the shards cover the global batch with the bench's per-instance slips."""
     import json
     port = _free_port()
     out = str(tmp_path / "bench")
     procs = [subprocess.Popen([sys.executable, "-c", BENCH_WORKER.format(root=ROOT, pkg=PKG_DIR, port=port, rank=r,
-                                                                          out=out)], cwd=ROOT) for r in range(2)]
+                                                                          out=out, world=world)], cwd=ROOT)
+             for r in range(world)]
     for p in procs:
         assert p.wait(timeout=240) == 0
-    res = [json.load(open(f"{out}.{r}.json")) for r in range(2)]
-    assert res[0]["emax"] == res[1]["emax"] == max(r["elapsed"] for r in res)
-    assert res[1]["elapsed"] >= 3 * 0.04
+    res = [json.load(open(f"{out}.{r}.json")) for r in range(world)]
+    assert all(r["emax"] == max(x["elapsed"] for x in res) for r in res)
+    assert res[-1]["elapsed"] >= 3 * 0.02 * world
     for r in res:
-        assert r["value"] == 4 * 2 * 3 / r["emax"] and abs(r["ms"] - r["emax"] / 3 * 1e3) < 1e-9
+        assert r["value"] == 4 * world * 3 / r["emax"] and abs(r["ms"] - r["emax"] / 3 * 1e3) < 1e-9
         assert r["done"] == [[0, False], [1, True], [2, True], [3, True]]
-    assert (res[0]["lo"], res[0]["hi"], res[1]["lo"], res[1]["hi"]) == (0, 4, 4, 8)
-    assert res[0]["slips"] + res[1]["slips"] == [0.1 + 0.2 * b / 8 for b in range(8)]
+    assert [(r["lo"], r["hi"]) for r in res] == [(4 * k, 4 * k + 4) for k in range(world)]
+    assert sum((r["slips"] for r in res), []) == [0.1 + 0.2 * b / (4 * world) for b in range(4 * world)]
 
 
 def test_gloo_gather_and_max(tmp_path):
