@@ -1,7 +1,8 @@
 """Dense-row path timings (IRLMX_LAYOUT_DENSE): per-sweep cost of the backward
-(streaming M once per instance on the VALU vs one rocBLAS dgemm over all B
+(streaming M once per instance on the VALU vs one fp64-MFMA GEMM over all B
 instances of a shared table), the forward, soft VI and VI, on random dense
-tables.  usage: python tools/diag/dense_bench.py [S ...]"""
+tables.  usage: python tools/diag/dense_bench.py [S ...]
+(round 2 also timed a rocBLAS dgemm here; round 3 removed the library)"""
 import os, sys, time
 ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 sys.path[:0] = [os.path.join(ROOT, "irl-maxent_amd")]
@@ -22,13 +23,12 @@ for S in sizes:
         r = rng.uniform(0.0, 1.0, (B, S))
         tm = ops.terminal_mask([S - 1], S, batch=B, device=dev)
         res = {}
-        for mode, env, eng in (("stream", "1000000", "mfma"), ("gemm-mfma", "1", "mfma"), ("gemm-rocblas", "1", "rocblas")):
+        for mode, env in (("stream", "1000000"), ("gemm-mfma", "1")):
             if B == 1 and mode != "stream":
                 continue
             if os.environ.get("MODES") and mode not in os.environ["MODES"].split(","):
                 continue
             os.environ["IRLMX_DENSE_GEMM_MIN"] = env
-            os.environ["IRLMX_DENSE_GEMM_ENGINE"] = eng
             ops.backward_maxent(mdp, r, tm); torch.cuda.synchronize()
             t = time.perf_counter(); pi = ops.backward_maxent(mdp, r, tm); torch.cuda.synchronize()
             dt = time.perf_counter() - t
@@ -37,7 +37,6 @@ for S in sizes:
                   f"{B * S * S * 8 * 2 * S / dt / 1e9 if mode == 'stream' else S * S * 8 * 2 * S / dt / 1e9:.0f} GB/s "
                   f"matrix stream, {2.0 * S * S * B * 2 * S / dt / 1e12:.2f} TFLOP/s", flush=True)
         os.environ.pop("IRLMX_DENSE_GEMM_MIN", None)
-        os.environ.pop("IRLMX_DENSE_GEMM_ENGINE", None)
         if B in (1, 16) and not os.environ.get("BACKWARD_ONLY"):
             pi = ops.backward_maxent(mdp, r, tm)
             p0 = np.zeros((B, S)); p0[:, 0] = 1.0
