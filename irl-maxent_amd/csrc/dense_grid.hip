@@ -207,17 +207,9 @@ __device__ inline int dg_plain(const DenseGridArgs& a, int b, int blk, unsigned 
 template <int MODE, int RB, int CPT>
 __global__ void __launch_bounds__(kDG) dense_grid_kernel(DenseGridArgs a) {
   const int S = a.S;
-  // XCD grouping (as the grid shape): workgroups are dealt round-robin over the
-  // 8 XCDs, so the workgroups of instance g + 8 j all come from XCD group g and
-  // its granules stay in one L2; the grid is padded to 8 equal groups
-  int lin = blockIdx.x;
-  if (a.xcd_group) {
-    const int grp = blockIdx.x % 8, kk = blockIdx.x / 8;
-    const int il = grp + 8 * (kk / a.bpi);
-    if (il >= a.nb) return;
-    lin = il * a.bpi + kk % a.bpi;
-  }
-  const int b = lin / a.bpi, blk = lin % a.bpi, tid = threadIdx.x;
+  int b, blk;
+  if (!dg_place(a, b, blk)) return;  // padding workgroup of an XCD-grouped grid
+  const int tid = threadIdx.x;
   const int wave = tid / kWave, lane = tid & (kWave - 1);
   __shared__ int resident, lflag;
   __shared__ double red[kDGWaves][RB];
@@ -267,32 +259,12 @@ __global__ void __launch_bounds__(kDG) dense_grid_kernel(DenseGridArgs a) {
   }
   const __amdgpu_buffer_rsrc_t rg = gran_rsrc(a.gran + (size_t)b * 4 * S, 32u * (unsigned)S);
   const unsigned salt = (a.salt & 0xFFFu) << 20;
-  // plain stores (kept in the XCD's L2) when every workgroup of the instance
-  // runs on one XCD -- found by exchanging XCC ids once (grid shape)
-  bool plain = false;
-  if (a.xcd_group) {
-    const __amdgpu_buffer_rsrc_t rx = gran_rsrc(a.xgran + (size_t)b * 2 * a.bpi, 16u * (unsigned)a.bpi);
-    unsigned xcc;
-    asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
-    xcc &= 0xFu;
-    const unsigned htag = salt | 0xFFFFFu;
-    if (tid == 0) gran_store(rx, (unsigned)blk * 16u, xcc, htag, false);
-    unsigned off[1] = {(unsigned)(tid < a.bpi ? tid : 0) * 16u};
-    unsigned long long v[1] = {xcc};
-    if (!gran_gather<1>(rx, rx, off, tid < a.bpi ? 1u : 0u, htag, v)) lflag = 1;
-    const unsigned long long diff = wave_or_u64(tid < a.bpi ? (v[0] ^ xcc) : 0ull);
-    if (lane == 0) mred[0][wave] = diff;
-    __syncthreads();
-    if (lflag) {
-      if (tid == 0) atomicOr(a.err, 1);
-      return;
-    }
-    unsigned long long any = 0ull;
-#pragma unroll
-    for (int i = 0; i < kDGWaves; ++i) any |= mred[0][i];
-    plain = any == 0ull;
-    __syncthreads();
+  const int pl = dg_plain(a, b, blk, salt, &mred[0][0], &lflag);
+  if (pl < 0) {
+    if (tid == 0) atomicOr(a.err, 1);
+    return;
   }
+  const bool plain = pl == 1;
   const long long total = MODE == kModeBwd ? 2LL * S - 1 : -1;  // collapsed sweeps (maxent.py:154)
   double delta = 0.0;
   unsigned long long gmax = 0ull;  // backward: max |zs_k| (ordered bits; inf / NaN above every finite value)
