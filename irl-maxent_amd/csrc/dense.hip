@@ -574,25 +574,27 @@ size_t lds_bytes(int S) { return (size_t)S * sizeof(double); }
 
 // The LDS-staged kernels take up to kDenseLdsMaxStates doubles (64 KiB) of dynamic
 // LDS on top of their static words: beyond the default limit, so the attribute is
-// raised once per device before the first staged launch.  A failure here leaves
-// the launch to fail, which the callers' hipGetLastError checks report.
-void lds_prep() {
-  static std::atomic<int> done[64];
+// raised once per device before the first staged launch.  If the runtime
+// refuses it, the in-place (unstaged) kernels run instead: same arithmetic in
+// the same order, so the same results, only without the LDS copy.
+bool lds_prep() {
+  static std::atomic<int> done[64];  // 0 unknown, 1 raised, 2 refused
   int dev = 0;
-  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64 || done[dev].load(std::memory_order_acquire)) return;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return false;
+  const int st = done[dev].load(std::memory_order_acquire);
+  if (st) return st == 1;
   const int bytes = (int)(kDenseLdsMaxStates * sizeof(double));
+  bool ok = true;
   for (const void* fn : {(const void*)&dense_fwd_sweep_kernel<true>, (const void*)&dense_bwd_sweep_kernel<true>,
                          (const void*)&dense_bwd_final_kernel<true>, (const void*)&dense_bellman_sweep_kernel<true>,
                          (const void*)&dense_bellman_finish_kernel<true>})
-    (void)hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, bytes);
-  done[dev].store(1, std::memory_order_release);
+    ok &= hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, bytes) == hipSuccess;
+  if (!ok) (void)hipGetLastError();  // the refusal is handled here; do not leave it for the launch checks
+  done[dev].store(ok ? 1 : 2, std::memory_order_release);
+  return ok;
 }
 
-bool lds_vec(const DenseView& d) {
-  const bool v = dense_lds_vec(d);
-  if (v) lds_prep();
-  return v;
-}
+bool lds_vec(const DenseView& d) { return dense_lds_vec(d) && lds_prep(); }
 }  // namespace
 
 void dense_rows_launch(const double* dense, int S, int A, double* P, double* M, hipStream_t st) {
