@@ -82,16 +82,22 @@ def parse(argv=None):
     ap.add_argument("--first-steps", type=int, default=FIRST_STEPS,
                     help="steps from theta0 reported in first_steps (0: off)")
     ap.add_argument("--cpu-sweeps", type=int, default=60, help="timed CPU sweeps per statement")
-    ap.add_argument("--full-run", action="store_true",
+    fr = ap.add_mutually_exclusive_group()
+    fr.add_argument("--full-run", dest="full_run", action="store_true", default=None,
                     help="also run irl to convergence (maxent.py:240-252, eps 1e-4) on a fresh copy of the workload and "
-                         "report it under full_run (not part of the headline)")
+                         "report it under full_run (not part of the headline); default on for config c3 (~11 s), "
+                         "off for the others (c4 ~130 s, c5 ~65 s)")
+    fr.add_argument("--no-full-run", dest="full_run", action="store_false")
     ap.add_argument("--full-run-eps", type=float, default=1e-4)
     ap.add_argument("--full-run-max-steps", type=int, default=20000, help="cap on gradient steps of the full run")
     ap.add_argument("--no-compact", action="store_true", help="full run without compacting converged instances")
     ap.add_argument("--profile", default=None,
                     help="profiles/<tag>_summary.json of a rocprofv3 run of this workload (default: newest); its "
                          "kernel average and PMC HBM bytes are reported beside the live figures")
-    return ap.parse_args(argv)
+    args = ap.parse_args(argv)
+    if args.full_run is None:
+        args.full_run = args.config == "c3" and not args.size and not args.batch
+    return args
 
 
 def _latest(pattern):

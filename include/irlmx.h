@@ -129,6 +129,21 @@ int irlmx_backward_maxent(const irlmx_mdp* mdp, const double* reward, const uint
                           size_t workspace_bytes, void* stream);
 
 /*
+ * The same backward pass in numpy's own floating-point order (no reference
+ * counterpart beyond maxent.py:142-159 itself): every p[a].dot(zs) summed as
+ * numpy's OpenBLAS dgemv_t sums it on a Haswell-family x86-64 host (lane
+ * accumulators by column % 4, fused multiply-adds, lane and block sums), then
+ * er * dot, the sequential action sum and za / zs -- so the policy is
+ * bit-identical to the reference's there (oracle/blas_order.c pins the order).
+ * No rescaling: it overflows to NaN where the reference does.
+ *   exp_reward [B][S]  np.exp(reward) as the reference computes it (maxent.py:142)
+ * Requires S <= 4096 and S % 4 in {0, 1} (every square grid); IRLMX_EINVAL otherwise.
+ */
+int irlmx_backward_maxent_numpy_order(const irlmx_mdp* mdp, const double* exp_reward,
+                                      const uint8_t* terminal, double* p_action, int32_t* status,
+                                      void* stream);
+
+/*
  * Forward expected-SVF sweep -- replaces maxent.expected_svf_from_policy
  * (reference src/maxent.py:63-114): d <- p0 + sum_a P'_a^T (pi_a * d) from d = 0
  * until max|delta| <= eps, where P' has the terminal rows cleared.

@@ -212,7 +212,7 @@ __global__ void __launch_bounds__(kDG) dense_grid_kernel(DenseGridArgs a) {
   const int tid = threadIdx.x;
   const int wave = tid / kWave, lane = tid & (kWave - 1);
   __shared__ int resident, lflag;
-  __shared__ double red[kDGWaves][RB];
+  __shared__ double red[2][kDGWaves][RB];  // by sweep parity (see the gather's note)
   __shared__ unsigned long long mred[2][kDGWaves];
   if (tid == 0) {
     resident = coresident(a.err + 1, a.n_resident) ? 1 : 0;
@@ -288,7 +288,7 @@ __global__ void __launch_bounds__(kDG) dense_grid_kernel(DenseGridArgs a) {
       }
       int row;
       const double sum = rows_sum<CH>(acc, lane, row);
-      if ((lane & (kWave / CH - 1)) == 0) red[wave][r0 + row] = sum;
+      if ((lane & (kWave / CH - 1)) == 0) red[k & 1][wave][r0 + row] = sum;
     }
     __syncthreads();
     if (k > 0) {
@@ -311,9 +311,9 @@ __global__ void __launch_bounds__(kDG) dense_grid_kernel(DenseGridArgs a) {
     // sweep k + 1 at this workgroup's rows
     if (tid < RB && row0 + tid < S) {
       const int e = (MODE == kModeBwd && a.rescale && k > 0) ? rescale_exponent(bits_double(gmax)) : 0;
-      double acc = red[0][tid];
+      double acc = red[k & 1][0][tid];
 #pragma unroll
-      for (int w = 1; w < kDGWaves; ++w) acc += red[w][tid];
+      for (int w = 1; w < kDGWaves; ++w) acc += red[k & 1][w][tid];
       const double nv = MODE == kModeFwd ? rc + acc                       // maxent.py:110
                                          : ldexp(__dmul_rn(rc, acc), e);  // maxent.py:155-156 (rescaled)
       const unsigned tag1 = salt | ((unsigned)(k + 1) & 0xFFFFFu);
@@ -321,9 +321,11 @@ __global__ void __launch_bounds__(kDG) dense_grid_kernel(DenseGridArgs a) {
     }
     ++k;
     // gather v_k, and its max |v_k - v_(k-1)| (forward) / max |v_k| (backward) for the next loop test.
-    // (red and mred[k & 1] are rewritten only after this gather, which needs this
-    // workgroup's own rows of v_k, i.e. after thread r < RB has read red; mred
-    // alternates so that a wave still reading the previous test's words is safe.)
+    // red and mred alternate by sweep parity: a wave whose columns hold none of
+    // this workgroup's rows can finish this gather (other workgroups' rows only)
+    // and write the next partials before the owners (wave 0) have read this
+    // sweep's; the slot it writes is the other one, and this one is rewritten
+    // only after the next barrier, which the owners reach after their read.
     {
       const unsigned tag = salt | ((unsigned)k & 0xFFFFFu);
       unsigned off[CPT];
@@ -415,7 +417,7 @@ __global__ void __launch_bounds__(kDG) dense_bellman_grid_kernel(DenseGridArgs a
   if (!dg_place(a, b, blk)) return;
   const int tid = threadIdx.x, wave = tid / kWave, lane = tid & (kWave - 1);
   __shared__ int resident, lflag;
-  __shared__ double red[kDGWaves][K];
+  __shared__ double red[2][kDGWaves][K];  // by sweep parity (dense_grid_kernel's note)
   __shared__ unsigned long long mred[2][kDGWaves];
   if (tid == 0) {
     resident = coresident(a.err + 1, a.n_resident) ? 1 : 0;
@@ -481,7 +483,7 @@ __global__ void __launch_bounds__(kDG) dense_bellman_grid_kernel(DenseGridArgs a
       }
       int row;
       const double sum = rows_sum<16>(acc, lane, row);
-      if ((lane & 3) == 0) red[wave][r0 + row] = sum;
+      if ((lane & 3) == 0) red[k & 1][wave][r0 + row] = sum;
     }
     __syncthreads();
     if (k > 0) {
@@ -500,9 +502,9 @@ __global__ void __launch_bounds__(kDG) dense_bellman_grid_kernel(DenseGridArgs a
 #pragma unroll
       for (int act = 0; act < AT; ++act) {
         if (act >= A) break;
-        double dot = red[0][act * RB + tid];
+        double dot = red[k & 1][0][act * RB + tid];
 #pragma unroll
-        for (int w = 1; w < kDGWaves; ++w) dot += red[w][act * RB + tid];
+        for (int w = 1; w < kDGWaves; ++w) dot += red[k & 1][w][act * RB + tid];
         if (SOFT) {
           qkeep[act] = __dadd_rn(rr, __dmul_rn(a.discount, dot));
           v = softmax2(v, qkeep[act]);  // maxent.py:329-333

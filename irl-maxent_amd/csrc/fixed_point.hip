@@ -470,6 +470,112 @@ __global__ void __launch_bounds__(1024) bwd_fused_kernel(BwdArgs a) {
   if (tid == 0) a.status[b] = IRLMX_OK;
 }
 
+// ---------------------------------------------------------------------------
+// backward pass in numpy's floating-point order (irlmx_backward_maxent_numpy_order)
+// ---------------------------------------------------------------------------
+//
+// maxent.py:142-159 with every rounding where numpy / OpenBLAS put it on a
+// Haswell-family x86-64 host (oracle/blas_order.c states and pins the order):
+// p[a].dot(zs) per action -- four lane accumulators by column % 4 over the
+// first S & ~3 columns (fma lanes for rows s < S & ~3, rounded-product lanes
+// for the last row when S % 4 == 1; blocks of 2048 columns), lane sum
+// (l0 + l2) + (l1 + l3), the last column fused on -- then er * dot rounded,
+// zs = ((za0 + za1) + za2) + za3, and za / zs after exactly 2 S sweeps.  No
+// rescaling: it overflows to NaN exactly where the reference does.  er is the
+// caller's np.exp(reward) (ocml's exp may differ from numpy's in the last bit).
+// One workgroup per instance; zs ping-pongs in LDS (S <= 4096).
+
+constexpr int kNpBlock = 2048;  // OpenBLAS dgemv_t NBMAX
+
+struct NpArgs {
+  Model m;
+  const double* er;     // [B][S] exp(reward), numpy's
+  const uint8_t* term;  // [B][S]
+  double* pi;           // [B][S][A]
+  int32_t* status;
+};
+
+// one lane term: fma lanes (dgemv_kernel_4x4) or product-then-add lanes (dgemv_kernel_4x1)
+__device__ inline void np_lane(double (&l)[2][4], int c, double v, double x, bool fused) {
+  double& acc = l[c >= kNpBlock ? 1 : 0][c & 3];
+  acc = fused ? fma(v, x, acc) : __dadd_rn(acc, __dmul_rn(v, x));
+}
+
+// p[a][s, :] . x in OpenBLAS dgemv_t order, from the row's stored entries in
+// ascending column order (zero entries are exact no-ops while x is finite)
+template <int LAYOUT>
+__device__ double np_row_dot(const Model& m, int b, int a, int s, const double* x) {
+  const int S = m.S, m1 = S & ~3;
+  const bool fused = s < m1;
+  double l[2][4] = {{0.0, 0.0, 0.0, 0.0}, {0.0, 0.0, 0.0, 0.0}};
+  double tail_v = 0.0;
+  bool tail = false;
+  auto put = [&](int c, double v) {
+    if (c < m1) np_lane(l, c, v, x[c], fused);
+    // S % 4 == 1: the one column c = S - 1 (an unused ELL slot may repeat it with value 0)
+    else if (!tail || v != 0.0) { tail = true; tail_v = v; }
+  };
+  if (LAYOUT == IRLMX_LAYOUT_STENCIL5) {
+    // ascending columns: -y, -x, self, +x, +y (k = 4, 2, 0, 1, 3)
+    constexpr int order[kStencilK] = {4, 2, 0, 1, 3};
+#pragma unroll
+    for (int i = 0; i < kStencilK; ++i) {
+      const int k = order[i];
+      if (stencil_valid(s, k, m.W, m.H)) put(stencil_nbr(s, k, m.W, m.H), row_val(m, b, a, k, s));
+    }
+  } else if (LAYOUT == IRLMX_LAYOUT_ELL) {
+    for (int k = 0; k < m.K; ++k) put(row_nbr(m, b, s, k), row_val(m, b, a, k, s));
+  } else {
+    const double* row = m.row_val + ((inst_of(m, b) * m.A + a) * (size_t)S + s) * S;
+    for (int c = 0; c < S; ++c) put(c, row[c]);
+  }
+  double y = __dadd_rn(0.0, __dadd_rn(__dadd_rn(l[0][0], l[0][2]), __dadd_rn(l[0][1], l[0][3])));
+  if (m1 > kNpBlock) y = __dadd_rn(y, __dadd_rn(__dadd_rn(l[1][0], l[1][2]), __dadd_rn(l[1][1], l[1][3])));
+  if (tail) y = fma(tail_v, x[S - 1], y);
+  return y;
+}
+
+template <int LAYOUT>
+__global__ void __launch_bounds__(1024) bwd_numpy_order_kernel(NpArgs a) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  const Model& m = a.m;
+  const int S = m.S, A = m.A;
+  const int b = blockIdx.x, tid = threadIdx.x, nt = blockDim.x;
+  double* zbuf[2] = {(double*)smem, (double*)smem + S};
+  int* bad = (int*)(zbuf[1] + S);  // [2] sticky: sweep k's output had a non-finite value (slot k & 1)
+  const double* er = a.er + (size_t)b * S;
+  double* pi = a.pi + (size_t)b * S * A;
+  for (int s = tid; s < S; s += nt) zbuf[0][s] = a.term[(size_t)b * S + s] ? 1.0 : 0.0;  // maxent.py:146-147
+  if (tid < 2) bad[tid] = 0;
+  __syncthreads();
+  const long long n = 2LL * S;  // maxent.py:154
+  for (long long it = 0; it < n; ++it) {
+    const double* zin = zbuf[it & 1];
+    double* zout = zbuf[(it & 1) ^ 1];
+    // a non-finite zs meets a zero entry of every dense row (0 * inf): the
+    // reference's next dots are all NaN (a DENSE row visits every column itself)
+    const bool poisoned = LAYOUT != IRLMX_LAYOUT_DENSE && it > 0 && bad[(it - 1) & 1];
+    bool nf = false;
+    for (int s = tid; s < S; s += nt) {
+      double z = 0.0;
+      for (int act = 0; act < A; ++act) {
+        const double dot = poisoned ? kNaN : np_row_dot<LAYOUT>(m, b, act, s, zin);
+        const double za = __dmul_rn(er[s], dot);                 // maxent.py:155
+        z = act == 0 ? za : __dadd_rn(z, za);                    // maxent.py:156
+        if (it == n - 1) pi[(size_t)s * A + act] = za;
+      }
+      zout[s] = z;
+      nf |= !isfinite(z);
+    }
+    if (nf) bad[it & 1] = 1;
+    __syncthreads();
+  }
+  const double* zs = zbuf[n & 1];
+  for (int s = tid; s < S; s += nt)
+    for (int act = 0; act < A; ++act) pi[(size_t)s * A + act] = pi[(size_t)s * A + act] / zs[s];  // maxent.py:159
+  if (tid == 0) a.status[b] = IRLMX_OK;
+}
+
 struct SoftArgs {
   Model m;
   const double* reward;
@@ -1881,6 +1987,32 @@ extern "C" int irlmx_backward_maxent(const irlmx_mdp* mdp, const double* reward,
   hipLaunchKernelGGL(bwd_final_kernel, g, dim3(kSweepThreads), 0, st, a, ws, collapsed, r3);
   e = hipGetLastError();
   return e == hipSuccess ? 0 : hip_fail(e, "backward");
+}
+
+extern "C" int irlmx_backward_maxent_numpy_order(const irlmx_mdp* mdp, const double* exp_reward,
+                                                 const uint8_t* terminal, double* p_action, int32_t* status,
+                                                 void* stream) {
+  if (int rc = validate(mdp)) return rc;
+  const Model m = make_model(mdp);
+  if (int rc = need_all("backward_maxent_numpy_order", {{exp_reward, "exp_reward"}, {terminal, "terminal"},
+                                                        {p_action, "p_action"}, {status, "status"}}))
+    return rc;
+  if (m.S > kFusedMaxStates || (m.S & 3) > 1) {
+    set_error("backward_maxent_numpy_order: numpy's order is restated for S <= %d with S %% 4 in {0, 1}, got S=%d",
+              kFusedMaxStates, m.S);
+    return IRLMX_EINVAL;
+  }
+  hipStream_t st = (hipStream_t)stream;
+  NpArgs a{m, exp_reward, terminal, p_action, status};
+  void (*fn)(NpArgs) = m.stencil ? bwd_numpy_order_kernel<IRLMX_LAYOUT_STENCIL5>
+                                 : (m.dense ? bwd_numpy_order_kernel<IRLMX_LAYOUT_DENSE>
+                                            : bwd_numpy_order_kernel<IRLMX_LAYOUT_ELL>);
+  const size_t lds = 2 * (size_t)m.S * sizeof(double) + 2 * sizeof(int);
+  hipError_t e = hipFuncSetAttribute((const void*)fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+  if (e != hipSuccess) return hip_fail(e, "hipFuncSetAttribute");
+  hipLaunchKernelGGL(fn, dim3(m.B), dim3(m.S >= 1024 ? 1024 : ((m.S + kWave - 1) / kWave) * kWave), lds, st, a);
+  e = hipGetLastError();
+  return e == hipSuccess ? 0 : hip_fail(e, "backward_maxent_numpy_order");
 }
 
 static int bellman_common(const irlmx_mdp* mdp, const double* reward, const double* phi, double discount,

@@ -90,6 +90,29 @@ def backward_maxent(mdp, reward, terminal, rescale=True):
     return pi
 
 
+def numpy_order_supported(mdp):
+    """Whether backward_maxent_numpy_order covers this model (S <= 4096, S % 4 in {0, 1})."""
+    S = mdp.n_states
+    return S <= 4096 and S % 4 in (0, 1)
+
+
+def backward_maxent_numpy_order(mdp, exp_reward, terminal):
+    """Local action probabilities [B, S, A] (maxent.py:119-159) in numpy's own
+    floating-point order (irlmx_backward_maxent_numpy_order): bit-identical to
+    the reference's on a Haswell-family OpenBLAS host, NaN where it overflows.
+    ``exp_reward`` is np.exp(reward) as the reference computes it (maxent.py:142)."""
+    lib = _lib.load()
+    B, S, A = mdp.batch, mdp.n_states, mdp.n_actions
+    er = _f64(exp_reward, mdp, (B, S))
+    term = terminal.to(device=mdp.device, dtype=torch.uint8).reshape(B, S).contiguous()
+    pi = torch.empty((B, S, A), dtype=torch.float64, device=mdp.device)
+    status = torch.empty(B, dtype=torch.int32, device=mdp.device)
+    _lib.check(lib.irlmx_backward_maxent_numpy_order(mdp.struct(), _lib.ptr(er), _lib.ptr(term), _lib.ptr(pi),
+                                                     _lib.ptr(status), _lib.stream_ptr(mdp.device)),
+               "backward_maxent_numpy_order")
+    return pi
+
+
 def forward_svf(mdp, p_initial, terminal, p_action, eps=1e-5, max_iter=0):
     """Expected state-visitation frequencies (maxent.py:63-114).
 

@@ -7,10 +7,17 @@ GPU through libirlmx.so (``irlmx.ops``); only the demonstration statistics,
 the feature products and the user's optimizer stay on the host, as in the
 reference's outer loop.
 
+The non-causal backward pass (local_action_probabilities and the backward
+half of compute_expected_svf / irl) runs in numpy's own floating-point order
+when the model allows it (S <= 4096 and S % 4 in {0, 1}: every square grid),
+so its policy is bit-identical to the reference's on a Haswell-family
+OpenBLAS host (ops.backward_maxent_numpy_order).
+
 Deliberate differences (documented in DESIGN.md):
-* The non-causal backward pass rescales its partition vector by powers of two
-  (ratio-exact), so it stays finite where the reference overflows to NaN
-  (about 13x13 at unit reward).  ``IRLMX_REFERENCE_OVERFLOW=1`` disables it.
+* Where the reference's backward pass overflows to NaN (about 13x13 at unit
+  reward) the drop-in reruns it with its partition vector rescaled by powers
+  of two (ratio-exact), so the policy stays finite.
+  ``IRLMX_REFERENCE_OVERFLOW=1`` keeps the reference's NaN instead.
 * ``p_transition`` may also be an ``irlmx.DeviceMDP`` already resident in HBM.
 """
 
@@ -95,18 +102,29 @@ def expected_svf_from_policy(p_transition, p_initial, terminal, p_action, eps=1e
     return _host(svf)
 
 
+def _backward(mdp, reward, term):
+    """The backward policy on the device: numpy's order where the model allows it
+    (bit-identical to the reference), the rescaled pass where that overflows."""
+    reward = np.asarray(reward.cpu().numpy() if torch.is_tensor(reward) else reward, dtype=np.float64)
+    if mdp.batch == 1 and ops.numpy_order_supported(mdp):
+        pi = ops.backward_maxent_numpy_order(mdp, np.exp(reward), term)   # er = np.exp(reward), maxent.py:142
+        if not _rescale() or bool(torch.isfinite(pi).all()):
+            return pi
+    return ops.backward_maxent(mdp, reward, term, rescale=_rescale())
+
+
 def local_action_probabilities(p_transition, terminal, reward):
     """Backward pass of MaxEnt IRL, 2*S sweeps (maxent.py:119-159)."""
     mdp = _model(p_transition)
     term = ops.terminal_mask(terminal, mdp.n_states, device=mdp.device)
-    return _host(ops.backward_maxent(mdp, reward, term, rescale=_rescale()))
+    return _host(_backward(mdp, reward, term))
 
 
 def compute_expected_svf(p_transition, p_initial, terminal, reward, eps=1e-5):
     """Backward pass then forward pass (maxent.py:162-193)."""
     mdp = _model(p_transition)
     term = ops.terminal_mask(terminal, mdp.n_states, device=mdp.device)
-    pi = ops.backward_maxent(mdp, reward, term, rescale=_rescale())
+    pi = _backward(mdp, reward, term)
     svf, _, _ = ops.forward_svf(mdp, p_initial, term, pi, eps)
     return _host(svf)
 
@@ -144,10 +162,9 @@ def irl(p_transition, features, terminal, trajectories, optim, init, eps=1e-4, e
     and the visitation frequencies (D2H) across PCIe.
     """
     mdp = _model(p_transition)
-    rescale = _rescale()
 
     def svf_fn(m, reward, term, p0):
-        pi = ops.backward_maxent(m, reward, term, rescale=rescale)
+        pi = _backward(m, reward, term)
         svf, _, _ = ops.forward_svf(m, p0, term, pi, eps_esvf)
         return _host(svf)
 

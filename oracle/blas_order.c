@@ -1,0 +1,98 @@
+/*
+ * TEST INFRASTRUCTURE (oracle) -- never linked into or called by the product.
+ *
+ * The reference's non-causal backward pass (src/maxent.py:140-159) restated in
+ * the exact floating-point order numpy 2.2 / OpenBLAS 0.3.29 give it on x86-64
+ * hosts whose OpenBLAS core is Haswell-family (Haswell, SkylakeX, Zen -- the
+ * DYNAMIC_ARCH kernels that share dgemv_t_4.c with the Haswell micro-kernel),
+ * single-threaded partition (OPENBLAS_NUM_THREADS=1, or any thread count for
+ * S <= 625).  Pinned bit for bit against the reference's own outputs
+ * (tests/golden/maxent_small.npz, config1.npz) and against np.dot on the host
+ * (tests/test_oracle_blas_order.py).  The order, established by probing np.dot
+ * with one-, two- and three-nonzero rows (fma vs. separately rounded sums):
+ *
+ *   maxent.py:155  p[a].dot(zs), p[a] C-contiguous S x S  ->  cblas dgemv,
+ *                  OpenBLAS dgemv_t on the column-major view; per output row s:
+ *     - the first m1 = S - S % 4 columns in blocks of 2048 (NBMAX); inside a
+ *       block four lane accumulators, lane = column % 4, starting at 0:
+ *         rows s <  S & ~3 (dgemv_kernel_4x4): lane = fma(a, x, lane)
+ *         rows s >= S & ~3 (dgemv_kernel_4x1): lane = lane + a * x (rounded product)
+ *       block sum (l0 + l2) + (l1 + l3); y = ((0 + block0) + block1) ...
+ *     - the remaining S % 4 columns: y = fma(a, x, y), ascending (S % 4 == 1;
+ *       S % 4 in {2, 3} use other kernels and are not restated: rejected)
+ *   maxent.py:155  er * dot        one rounded product
+ *   maxent.py:156  za.sum(axis=1)  ((za0 + za1) + za2) + za3, sequential
+ *   maxent.py:159  za / zs         IEEE division
+ *
+ * Zero entries contribute fma(0, x, acc) = acc exactly while x is finite; a
+ * non-finite partition value makes every later dot NaN (0 * inf), which the
+ * dense restatement below reproduces by running over all S columns.
+ */
+
+#include <math.h>
+#include <stddef.h>
+#include <stdint.h>
+#include <stdlib.h>
+
+#define NBMAX 2048
+
+/* y[s] = sum_t M[s][t] x[t], M row-major n x n, in OpenBLAS Haswell dgemv_t order. */
+int blas_order_dgemv_rows(const double* M, int n, const double* x, double* y) {
+  if (n <= 0 || (n & 3) > 1) return -1;
+  const int m1 = n - (n & 3), n4 = n & ~3;
+  for (int s = 0; s < n; ++s) {
+    const double* a = M + (size_t)s * n;
+    const int fused = s < n4;
+    double out = 0.0;
+    for (int lo = 0; lo < m1; lo += NBMAX) {
+      const int hi = lo + NBMAX < m1 ? lo + NBMAX : m1;
+      double l[4] = {0.0, 0.0, 0.0, 0.0};
+      for (int t = lo; t < hi; ++t) {
+        const int q = (t - lo) & 3;
+        l[q] = fused ? fma(a[t], x[t], l[q]) : l[q] + a[t] * x[t];
+      }
+      out = out + ((l[0] + l[2]) + (l[1] + l[3]));
+    }
+    for (int t = m1; t < n; ++t) out = fma(a[t], x[t], out);
+    y[s] = out;
+  }
+  return 0;
+}
+
+/*
+ * local_action_probabilities (maxent.py:119-159) in that order.
+ *   P  [S][S][A] C order (the reference's p_transition), term [S] (1 = terminal),
+ *   er [S] = np.exp(reward) computed by the caller with numpy (maxent.py:142),
+ *   pi [S][A] out.
+ */
+int blas_order_backward_maxent(const double* P, int S, int A, const uint8_t* term, const double* er,
+                               double* pi) {
+  if (S <= 0 || A <= 0 || (S & 3) > 1) return -1;
+  double* pa = malloc((size_t)A * S * S * sizeof(double));
+  double* zs = malloc((size_t)S * sizeof(double));
+  double* dot = malloc((size_t)S * sizeof(double));
+  double* za = malloc((size_t)S * A * sizeof(double));
+  if (!pa || !zs || !dot || !za) {
+    free(pa); free(zs); free(dot); free(za);
+    return -2;
+  }
+  for (int a = 0; a < A; ++a)  /* maxent.py:143: the C-contiguous slices p[a] */
+    for (int s = 0; s < S; ++s)
+      for (int t = 0; t < S; ++t) pa[((size_t)a * S + s) * S + t] = P[((size_t)s * S + t) * A + a];
+  for (int s = 0; s < S; ++s) zs[s] = term[s] ? 1.0 : 0.0;  /* maxent.py:146-147 */
+  for (int it = 0; it < 2 * S; ++it) {                      /* maxent.py:154 */
+    for (int a = 0; a < A; ++a) {
+      blas_order_dgemv_rows(pa + (size_t)a * S * S, S, zs, dot);
+      for (int s = 0; s < S; ++s) za[(size_t)s * A + a] = er[s] * dot[s];
+    }
+    for (int s = 0; s < S; ++s) {
+      double z = za[(size_t)s * A];
+      for (int a = 1; a < A; ++a) z = z + za[(size_t)s * A + a];
+      zs[s] = z;
+    }
+  }
+  for (int s = 0; s < S; ++s)
+    for (int a = 0; a < A; ++a) pi[(size_t)s * A + a] = za[(size_t)s * A + a] / zs[s];
+  free(pa); free(zs); free(dot); free(za);
+  return 0;
+}

@@ -72,13 +72,19 @@ def _vi(lib, m, a):
                                      a["ws"], a["n"], NULL)
 
 
+def _bwd_np(lib, m, a):
+    return lib.irlmx_backward_maxent_numpy_order(m, a["exp_reward"], a["terminal"], a["p_action"], a["status"], NULL)
+
+
 ENTRY = {
     "backward_maxent": (1, _bwd, ("reward", "terminal", "p_action", "status")),
+    "backward_maxent_numpy_order": (1, _bwd_np, ("exp_reward", "terminal", "p_action", "status")),
     "forward_svf": (2, _fwd, ("p_initial", "terminal", "p_action", "svf", "iterations", "status")),
     "soft_backward": (3, _soft, ("reward", "terminal_reward", "p_action", "iterations", "status")),
     "value_iteration": (4, _vi, ("reward", "value", "iterations", "status")),
 }
-ARGS = ("reward", "terminal", "p_action", "status", "p_initial", "svf", "iterations", "terminal_reward", "value")
+ARGS = ("reward", "terminal", "p_action", "status", "p_initial", "svf", "iterations", "terminal_reward", "value",
+        "exp_reward")
 
 
 def args_for(lib, m, op, **over):
@@ -147,7 +153,7 @@ def test_optional_arrays_accepted_as_null(lib):
     assert _soft(lib, ctypes.byref(m), a) == EWORKSPACE
 
 
-@pytest.mark.parametrize("fn", sorted(ENTRY))
+@pytest.mark.parametrize("fn", sorted(set(ENTRY) - {"backward_maxent_numpy_order"}))  # (takes no workspace)
 @pytest.mark.parametrize("layout", ["stencil", "ell", "dense"])
 def test_workspace_too_small(lib, fn, layout):
     op, call, _ = ENTRY[fn]
@@ -240,3 +246,13 @@ def test_counters_and_python_errors(lib):
     rc = _bwd(lib, ctypes.byref(m), args_for(lib, model(), 1))
     with pytest.raises(_lib.IrlmxError, match=r"backward_maxent failed \(-1\): bad sizes S=0"):
         _lib.check(rc, "backward_maxent")
+
+
+@pytest.mark.parametrize("S,W,H", [(6, 2, 3), (7, 7, 1), (4097, 4097, 1), (65 * 65, 65, 65)])
+def test_numpy_order_sizes_einval(lib, S, W, H):
+    """numpy's order is restated for S <= 4096 with S % 4 in {0, 1} only
+    (oracle/blas_order.c): other sizes are rejected, not approximated."""
+    m = model(S=S, W=W, H=H)
+    a = args_for(lib, model(), 1)
+    assert _bwd_np(lib, ctypes.byref(m), a) == EINVAL
+    assert "numpy's order is restated for S <= 4096" in err(lib), err(lib)

@@ -78,3 +78,14 @@ def test_timed_steps_brackets_exactly_k_steps():
     assert log.count("barrier") == 2
     v, ms = bench.headline(elapsed, 64, 2, 3)
     assert v == 64 * 2 * 3 / 12.0 and ms == 4000.0
+
+
+def test_full_run_default():
+    """The default bench line (config 3) also runs irl to convergence (full_run);
+    the long configs and overridden workloads only on request."""
+    import bench
+    assert bench.parse([]).full_run is True
+    assert bench.parse(["--no-full-run"]).full_run is False
+    assert bench.parse(["--config", "c4"]).full_run is False
+    assert bench.parse(["--config", "c5", "--full-run"]).full_run is True
+    assert bench.parse(["--size", "64"]).full_run is False

@@ -1,0 +1,199 @@
+"""Argmax / policy indices end to end, device only (needs an MI355X).
+
+North star: "bit-exact on indices/argmax".  These tests never feed the device
+a reference value vector: every index below comes from a chain that runs on
+the device from the reward, compared with the reference's own output
+(tests/golden, made by importing the reference, tools/gen_golden.py).
+
+* Greedy policy (solver.py:107-152): device value_iteration -> device
+  optimal_policy_from_value, and the drop-in solver.optimal_policy(world, ...),
+  against the reference's ``opt_policy`` -- np.array_equal, ties (first index)
+  included (det4 has nine states with two exactly tied successors).
+* Argmax of the backward policy (maxent.py:159, 341) at every reference-pinned
+  case, ties included (see test_backward_policy_argmax for how ties are
+  reproduced).
+"""
+
+import numpy as np
+import pytest
+
+import maxent_oracle as O
+from conftest import load_golden
+
+pytestmark = pytest.mark.gpu
+
+torch = pytest.importorskip("torch")
+
+
+@pytest.fixture(scope="module")
+def dev():
+    import __graft_entry__ as g
+    g.build()
+    import irlmx
+    return irlmx.require_device()
+
+
+class GridWorldStandIn:
+    """The reference GridWorld API solver.optimal_policy uses (gridworld.py:14-122):
+    size, actions, n_states / n_actions, state_index_transition, p_transition."""
+
+    def __init__(self, size, p_transition):
+        self.size = size
+        self.n_states, self.n_actions = size * size, 4
+        self.actions = O.ACTIONS
+        self.p_transition = p_transition
+
+    def state_index_transition(self, s, a):
+        return O.intended_successor(self.size, s, a)
+
+
+def _argmax_report(got, ref):
+    bad = np.flatnonzero(got != ref)
+    return f"{bad.size} states differ: " + ", ".join(f"s={s} got {got[s]} ref {ref[s]}" for s in bad[:8])
+
+
+def test_value_iteration_policy_chain(dev):
+    """solver.optimal_policy (solver.py:127-152) = value_iteration on the device,
+    then the greedy successor argmax on the device, for every golden VI case with
+    a greedy policy (5x5 and 16x16, discount 0.7 / 0.9) and det4 (deterministic
+    4x4 GridWorld, discount 0.5, nine states with exact two-way ties)."""
+    import solver as S
+    from irlmx import DeviceMDP, ops
+    z = load_golden("vi")
+    cases = [str(c) for c in z["names"] if str(c) + "__opt_policy" in z]
+    assert len(cases) == 4
+    for c in cases:
+        size = int(z[c + "__size"])
+        mdp = DeviceMDP.icy_gridworld(size, 0.2, device=dev)
+        v, k, _ = ops.value_iteration(mdp, z[c + "__reward"], float(z[c + "__discount"]))
+        assert int(k[0]) == int(z[c + "__k"]), c
+        succ = torch.as_tensor(S.successor_table(GridWorldStandIn(size, None)), device=dev)
+        pol = ops.optimal_policy(succ, v[0]).cpu().numpy()[0]
+        assert np.array_equal(pol, z[c + "__opt_policy"]), (c, _argmax_report(pol, z[c + "__opt_policy"]))
+        # the drop-in path: numpy table in, numpy indices out
+        world = GridWorldStandIn(size, O.icy_gridworld_table(size, 0.2))
+        pol2 = S.optimal_policy(world, z[c + "__reward"], float(z[c + "__discount"]))
+        assert np.array_equal(pol2, z[c + "__opt_policy"]), (c, _argmax_report(pol2, z[c + "__opt_policy"]))
+    world = GridWorldStandIn(4, O.gridworld_table(4))
+    mdp = DeviceMDP.gridworld(4, device=dev)
+    v, k, _ = ops.value_iteration(mdp, z["det4__reward"], 0.5)
+    assert int(k[0]) == int(z["det4__k"])
+    assert np.array_equal(v[0].cpu().numpy(), z["det4__value"])   # deterministic moves: exact arithmetic
+    succ = torch.as_tensor(S.successor_table(world), device=dev)
+    pol = ops.optimal_policy(succ, v[0]).cpu().numpy()[0]
+    assert np.array_equal(pol, z["det4__opt_policy"]), _argmax_report(pol, z["det4__opt_policy"])
+    pol2 = S.optimal_policy(world, z["det4__reward"], 0.5)
+    assert np.array_equal(pol2, z["det4__opt_policy"]), _argmax_report(pol2, z["det4__opt_policy"])
+
+
+def test_config1_policy_chain(dev):
+    """BASELINE config 1 (src/main.py): the expert's greedy policy from the
+    device's own value iteration equals the reference's."""
+    import solver as S
+    z = load_golden("config1")
+    world = GridWorldStandIn(5, z["p_transition"])
+    pol = S.optimal_policy(world, z["reward"], 0.7)
+    assert np.array_equal(pol, z["opt_policy"]), _argmax_report(pol, z["opt_policy"])
+
+
+def _pinned_backward_cases():
+    """(name, p_transition, terminal, reward, reference pi) of every reference-pinned
+    backward-policy case with a finite reference policy: maxent_small (5x5 - 12x12),
+    config 1's pi1 (maxent.py:159)."""
+    z = load_golden("maxent_small")
+    for c in [str(n) for n in z["names"]]:
+        if not np.isfinite(z[c + "__pi"]).all():
+            continue
+        P = O.icy_gridworld_table(int(z[c + "__size"]), float(z[c + "__p_slip"]))
+        yield c, P, [int(t) for t in z[c + "__terminal"]], z[c + "__reward"], z[c + "__pi"]
+    z = load_golden("config1")
+    yield "config1_pi1", z["p_transition"], [int(t) for t in z["terminal"]], np.ones(25), z["pi1"]
+
+
+def _pinned_causal_cases():
+    z = load_golden("causal_small")
+    for c in [str(n) for n in z["names"]]:
+        size = int(z[c + "__size"])
+        yield (c, O.icy_gridworld_table(size, 0.2), [int(t) for t in z[c + "__terminal"]], z[c + "__reward"],
+               float(z[c + "__discount"]), z[c + "__pi"])
+    z = load_golden("config1")
+    yield "config1_cpi1", z["p_transition"], [int(t) for t in z["terminal"]], np.ones(25), 0.7, z["cpi1"]
+
+
+def test_backward_policy_argmax(dev):
+    """The drop-in maxent.local_action_probabilities runs the backward pass in
+    numpy's own floating-point order (irlmx_backward_maxent_numpy_order), so the
+    policy -- and with it every argmax, the 1-ulp near-ties of the unit-reward
+    cases included -- is bit-identical to the reference's output."""
+    import maxent as M
+    for name, P, term, r, ref in _pinned_backward_cases():
+        pi = M.local_action_probabilities(P, term, r)
+        assert np.array_equal(pi, ref), (name, np.max(np.abs(pi - ref)))
+        got, want = np.argmax(pi, axis=1), np.argmax(ref, axis=1)
+        assert np.array_equal(got, want), (name, _argmax_report(got, want))
+
+
+def test_numpy_order_all_layouts_and_overflow(dev, monkeypatch):
+    """ops.backward_maxent_numpy_order on the STENCIL5, ELL and DENSE layouts
+    against the reference's output bit for bit, every maxent_small case: the
+    overflowing ones give the reference's NaN pattern (no rescaling), and the
+    drop-in then reruns them rescaled unless IRLMX_REFERENCE_OVERFLOW=1."""
+    import maxent as M
+    from irlmx import DeviceMDP, ops
+    z = load_golden("maxent_small")
+    for c in [str(n) for n in z["names"]]:
+        size = int(z[c + "__size"])
+        n = size * size
+        P = O.icy_gridworld_table(size, float(z[c + "__p_slip"]))
+        term = [int(t) for t in z[c + "__terminal"]]
+        ref = z[c + "__pi"]
+        tm = ops.terminal_mask(term, n, device=dev)
+        er = np.exp(z[c + "__reward"])
+        for layout in ("stencil", "ell", "dense"):
+            mdp = DeviceMDP.from_dense(P, device=dev, layout=layout)
+            pi = ops.backward_maxent_numpy_order(mdp, er, tm)[0].cpu().numpy()
+            assert np.array_equal(pi, ref, equal_nan=True), (c, layout)
+        if not np.isfinite(ref).all():
+            monkeypatch.setenv("IRLMX_REFERENCE_OVERFLOW", "1")
+            assert np.array_equal(M.local_action_probabilities(P, term, z[c + "__reward"]), ref, equal_nan=True)
+            monkeypatch.delenv("IRLMX_REFERENCE_OVERFLOW")
+            if term:   # rescaled rerun: the oracle's ratio-exact rescaled pass
+                pi = M.local_action_probabilities(P, term, z[c + "__reward"])
+                ro = O.backward_maxent(P, term, z[c + "__reward"], rescale=True)
+                assert np.isfinite(pi).all() and np.max(np.abs(pi - ro)) <= 1e-8 * np.max(np.abs(ro)), c
+
+
+def test_numpy_order_generic_and_batched(dev):
+    """Non-grid MDPs (tests/golden/generic.npz: sparse, dense and five-action
+    tables, S = 20 / 12 / 40) against the C restatement of numpy's order, and a
+    batch of instances with per-instance tables and rewards equal to single calls."""
+    from irlmx import DeviceMDP, ops
+    g = load_golden("generic")
+    for c in [str(n) for n in g["names"]]:
+        P = g[c + "__P"]
+        term = [int(t) for t in g[c + "__terminal"]]
+        r = g[c + "__reward"]
+        ref = O.backward_maxent_blas_order(P, term, r)
+        assert np.array_equal(ref, O.backward_maxent(P, term, r), equal_nan=True), c   # numpy itself, this host
+        for layout in ("ell", "dense"):
+            mdp = DeviceMDP.from_dense(P, device=dev, layout=layout)
+            pi = ops.backward_maxent_numpy_order(mdp, np.exp(r), ops.terminal_mask(term, P.shape[0], device=dev))
+            assert np.array_equal(pi[0].cpu().numpy(), ref, equal_nan=True), (c, layout)
+    size, B = 9, 3
+    n = size * size
+    slips = [0.1, 0.2, 0.35]
+    rng = np.random.default_rng(4)
+    r = rng.uniform(-0.5, 0.3, (B, n))
+    mdp = DeviceMDP.icy_gridworld(size, slips, device=dev)
+    pi = ops.backward_maxent_numpy_order(mdp, np.exp(r), ops.terminal_mask([n - 1], n, batch=B, device=dev))
+    for b in range(B):
+        ref = O.backward_maxent_blas_order(O.icy_gridworld_table(size, slips[b]), [n - 1], r[b])
+        assert np.array_equal(pi[b].cpu().numpy(), ref, equal_nan=True), b
+
+
+def test_causal_policy_argmax(dev):
+    import maxent as M
+    for name, P, term, r, g, ref in _pinned_causal_cases():
+        pi = M.local_causal_action_probabilities(P, term, r, g)
+        got, want = np.argmax(pi, axis=1), np.argmax(ref, axis=1)
+        assert np.array_equal(got, want), (name, _argmax_report(got, want))
