@@ -459,6 +459,12 @@ def full_run(args, mdp, e_f, p_0, terminal, causal, dev, barrier, world):
     }
 
 
+def rank_device(local_rank, n_devices):
+    """The GPU of a rank: one per rank (LOCAL_RANK); more ranks than GPUs (a
+    rehearsal of the multi-rank path on a 1-GPU box) share them round-robin."""
+    return local_rank % max(1, n_devices)
+
+
 def main(argv=None):
     args = parse(argv)
     # stdout carries exactly one JSON line: whatever libraries print there (gloo's
@@ -478,9 +484,7 @@ def main(argv=None):
         # host-side group: only the timing barrier and the max-over-ranks travel
         # (no data-path collective) -- RCCL is not needed
         dist.init_process_group(backend="gloo")
-    # one GPU per rank; more ranks than GPUs (a rehearsal of the multi-rank path
-    # on a 1-GPU box) share them round-robin
-    local = local % max(1, torch.cuda.device_count())
+    local = rank_device(local, torch.cuda.device_count())
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
 

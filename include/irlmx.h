@@ -112,6 +112,20 @@ const char* irlmx_last_error(void);
 #define IRLMX_CTR_SWEEP_CALLS 5        /* calls (or reruns) that took the per-sweep shape */
 int irlmx_counters(int64_t* out, int32_t n);
 
+/*
+ * Device bounds checks (diagnostics; no reference
+ * counterpart).  A library built with -DIRLMX_DEVICE_CHECKS=1 checks, inside the
+ * kernels, every ELL slot index against [0, S), every halo / value granule
+ * offset against its buffer, and every persistent tile's row range against the
+ * grid and its LDS buffer; a failed check skips the access and sets a bit
+ * (1: index, 2: granule, 4: tile) instead of faulting.
+ * irlmx_device_check_failures() synchronises the device and returns the bits
+ * set since the last call (then clears them); always 0 in a normal build
+ * (irlmx_device_checks_enabled() == 0), -1 on a HIP error.
+ */
+int irlmx_device_checks_enabled(void);
+int64_t irlmx_device_check_failures(void);
+
 /* Bytes of device workspace `op` needs for this model (0 is a valid answer). */
 size_t irlmx_workspace_bytes(const irlmx_mdp* mdp, int32_t op);
 
@@ -176,6 +190,26 @@ int irlmx_soft_backward(const irlmx_mdp* mdp, const double* reward, const double
 int irlmx_value_iteration(const irlmx_mdp* mdp, const double* reward, double discount, double eps,
                           int32_t average, int64_t max_iter, double* value, int64_t* iterations,
                           int32_t* status, void* workspace, size_t workspace_bytes, void* stream);
+
+/*
+ * Soft value iteration and value iteration in numpy's own floating-point order
+ * (no reference counterpart beyond maxent.py:326-341 / solver.py:40-50, 95-100
+ * themselves): every p[a].dot(v) / p[a] @ v summed as numpy's OpenBLAS dgemv_t
+ * sums it on a Haswell-family x86-64 host (see
+ * irlmx_backward_maxent_numpy_order), then the same statements as
+ * irlmx_soft_backward / irlmx_value_iteration.  Value iteration has no
+ * transcendental function: its values and sweep counts are bit-identical to the
+ * reference's there.  Soft VI's exp / log are the device's (numpy's SIMD exp /
+ * log may differ in the last bit): its dot products, and with them the
+ * mirror-symmetric ties of its policy, follow numpy.  No workspace.
+ * Requires S <= 4096 and S % 4 in {0, 1}; IRLMX_EINVAL otherwise.
+ */
+int irlmx_soft_backward_numpy_order(const irlmx_mdp* mdp, const double* reward, const double* terminal_reward,
+                                    double discount, double eps, int64_t max_iter, double* p_action,
+                                    double* value, int64_t* iterations, int32_t* status, void* stream);
+int irlmx_value_iteration_numpy_order(const irlmx_mdp* mdp, const double* reward, double discount, double eps,
+                                      int32_t average, int64_t max_iter, double* value, int64_t* iterations,
+                                      int32_t* status, void* stream);
 
 /*
  * Execution plan a call of `op` (IRLMX_OP_*) on this model would run, without

@@ -6,6 +6,7 @@
 #include <atomic>
 #include <cstdarg>
 #include <cstdio>
+#include <vector>
 
 #include "common.h"
 
@@ -31,7 +32,27 @@ void count_event(int which) {
   if (which >= 0 && which < IRLMX_COUNTERS_LEN) g_counters[which].fetch_add(1, std::memory_order_relaxed);
 }
 
+static std::vector<DcheckTake>& dcheck_registry() {
+  static std::vector<DcheckTake> r;
+  return r;
+}
+
+bool register_dcheck(DcheckTake take) {
+  dcheck_registry().push_back(take);
+  return true;
+}
+
 }  // namespace irlmx
+
+extern "C" int irlmx_device_checks_enabled(void) { return IRLMX_DEVICE_CHECKS; }
+
+extern "C" int64_t irlmx_device_check_failures(void) {
+  if (!IRLMX_DEVICE_CHECKS) return 0;
+  if (hipDeviceSynchronize() != hipSuccess) return -1;
+  unsigned v = 0;
+  for (auto take : irlmx::dcheck_registry()) v |= take();
+  return (int64_t)v;
+}
 
 extern "C" int irlmx_abi_version(void) { return IRLMX_ABI_VERSION; }
 

@@ -75,16 +75,32 @@ typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
 #endif
 constexpr int kGatherPerThread = 4;
 
-__device__ inline __amdgpu_buffer_rsrc_t gran_rsrc(const void* base, unsigned bytes) {
-  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), 0, (int)bytes, 0x00020000);
+// A granule buffer: its descriptor (and, in IRLMX_DEVICE_CHECKS builds, its
+// byte length for the offset checks).
+struct Gran {
+  __amdgpu_buffer_rsrc_t r;
+#if IRLMX_DEVICE_CHECKS
+  unsigned bytes;
+#endif
+};
+__device__ inline Gran gran_rsrc(const void* base, unsigned bytes) {
+  Gran g;
+  g.r = __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), 0, (int)bytes, 0x00020000);
+#if IRLMX_DEVICE_CHECKS
+  g.bytes = bytes;
+#endif
+  return g;
 }
+#if IRLMX_DEVICE_CHECKS
+__device__ inline bool gran_in(const Gran& g, unsigned off) { return g.bytes >= 16u && off <= g.bytes - 16u; }
+#endif
 __device__ inline unsigned long long dbits(double v) { return (unsigned long long)__double_as_longlong(v); }
 // sc1 (write-through) store, or a plain store when every reader shares this XCD's L2
-__device__ inline void gran_store(__amdgpu_buffer_rsrc_t r, unsigned off, unsigned long long v, unsigned tag,
-                                  bool plain) {
+__device__ inline void gran_store(const Gran& g, unsigned off, unsigned long long v, unsigned tag, bool plain) {
+  if (!IRLMX_DCHECK(gran_in(g, off), kCheckGranule)) return;
   const u32x4 x = {(unsigned)v, tag, (unsigned)(v >> 32), tag};
-  if (plain) __builtin_amdgcn_raw_buffer_store_b128(x, r, (int)off, 0, 0);
-  else __builtin_amdgcn_raw_buffer_store_b128(x, r, (int)off, 0, 16 /* sc1 */);
+  if (plain) __builtin_amdgcn_raw_buffer_store_b128(x, g.r, (int)off, 0, 0);
+  else __builtin_amdgcn_raw_buffer_store_b128(x, g.r, (int)off, 0, 16 /* sc1 */);
 }
 // Poll the granule pairs selected by `want` (bit k: entry k; the last entry
 // through rsrc `rl`, the others through `r`) until all carry `tag`; false
@@ -93,18 +109,27 @@ __device__ inline void gran_store(__amdgpu_buffer_rsrc_t r, unsigned off, unsign
 constexpr unsigned long long kGatherTicks = 2000000000ull;
 // (mask type M: 32-bit, or 64-bit for more than 32 entries)
 template <int N, typename M>
-__device__ inline bool gran_gather(__amdgpu_buffer_rsrc_t r, __amdgpu_buffer_rsrc_t rl, const unsigned (&off)[N],
+__device__ inline bool gran_gather(const Gran& r, const Gran& rl, const unsigned (&off)[N],
                                    M want, unsigned tag, unsigned long long (&v)[N],
                                    unsigned long long limit = kGatherTicks) {
   static_assert(N <= 8 * (int)sizeof(M), "gran_gather: mask too narrow");
   M pending = want;
+#if IRLMX_DEVICE_CHECKS
+#pragma unroll
+  for (int k = 0; k < N; ++k) {
+    if (((pending >> k) & 1u) && !IRLMX_DCHECK(gran_in(k == N - 1 ? rl : r, off[k]), kCheckGranule)) {
+      pending &= ~((M)1 << k);  // skipped: the value reads as 0
+      v[k] = 0ull;
+    }
+  }
+#endif
   const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
   while (pending) {
     u32x4 x[N];
 #pragma unroll
     for (int k = 0; k < N; ++k)
       if ((pending >> k) & 1u)
-        x[k] = __builtin_amdgcn_raw_buffer_load_b128(k == N - 1 ? rl : r, (int)off[k], 0, 16 /* sc1 */);
+        x[k] = __builtin_amdgcn_raw_buffer_load_b128(k == N - 1 ? rl.r : r.r, (int)off[k], 0, 16 /* sc1 */);
 #pragma unroll
     for (int k = 0; k < N; ++k)
       if (((pending >> k) & 1u) && x[k].y == tag && x[k].w == tag) {

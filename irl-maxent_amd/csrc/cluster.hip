@@ -142,6 +142,12 @@ __global__ void __launch_bounds__(NT) cluster_kernel(ClusterArgs a) {
   const int r0 = tile * a.R, r1 = min(H, r0 + a.R);
   const int e0 = max(0, r0 - a.G), e1 = min(H, r1 + a.G);
   const int E = (e1 - e0) * W;
+  // device checks: the tile's rows inside the grid, its extended tile inside the
+  // LDS buffer and the register slots (a failing workgroup leaves; its
+  // neighbours' exchange then times out and the host reruns per sweep)
+  if (!IRLMX_DCHECK(0 <= e0 && e0 <= r0 && r0 < r1 && r1 <= e1 && e1 <= H && E <= a.emax && E <= SPT * NT,
+                    kCheckTile))
+    return;
   const int own0 = (r0 - e0) * W, own1 = (r1 - e0) * W;
   // owned rows other tiles read as ghosts: within G rows of either tile edge
   const int pubA1 = min(own1, own0 + a.G * W), pubB0 = max(pubA1, own1 - a.G * W);
@@ -381,15 +387,21 @@ __global__ void __launch_bounds__(NT) cluster_kernel(ClusterArgs a) {
       // x = 0 and lane HW - 1 is x = W - 1, whose out-of-row neighbour (weight 0)
       // reads an adjacent, finite array entry.
       double side[2][2];  // [top, bottom][left, right]
-      auto edges_in = [&]() {
-        __syncthreads();
+      // (which: 1 = the row above, 2 = the row below, 3 = both; sync: the barrier first)
+      auto edges_in = [&](int which = 3, bool sync = true) {
+        if (sync) __syncthreads();
         const double2* t = bnd_at(i & 1, bb, 1);
         const double2* u = bnd_at(i & 1, bb + 2, 0);
 #pragma unroll
         for (int q = 0; q < QW; ++q) {
-          const double2 x = t[q], y = u[q];
-          above[2 * q] = x.x; above[2 * q + 1] = x.y;
-          below[2 * q] = y.x; below[2 * q + 1] = y.y;
+          if (which & 1) {
+            const double2 x = t[q];
+            above[2 * q] = x.x; above[2 * q + 1] = x.y;
+          }
+          if (which & 2) {
+            const double2 y = u[q];
+            below[2 * q] = y.x; below[2 * q + 1] = y.y;
+          }
         }
         if constexpr (kLdsSides) {
 #pragma unroll
@@ -440,17 +452,27 @@ __global__ void __launch_bounds__(NT) cluster_kernel(ClusterArgs a) {
       constexpr int step = CPL == 2 ? 2 : 1;
       constexpr int n_int = RW >= 3 ? (RW - 2 + step - 1) / step : 0;
       constexpr int kPre = (n_int + 1) / 2;
+      // IRLMX_QUAD_LAZY_ABOVE (quads): the row below is read at the barrier, the
+      // row above only before the band's top row, so the two edge rows are never
+      // live together (four doubles less register pressure; the hot loop has no
+      // scratch either way -- DESIGN.md section 4 "Registers").
+#ifndef IRLMX_QUAD_LAZY_ABOVE
+#define IRLMX_QUAD_LAZY_ABOVE 0
+#endif
+      constexpr bool kLazy = CPL == 4 && IRLMX_QUAD_LAZY_ABOVE;
+      constexpr int kFirst = kLazy ? 2 : 3;
 #pragma unroll
       for (int s = 0; s < n_int; ++s) {
-        if (s == kPre) edges_in();
+        if (s == kPre) edges_in(kFirst);
         const int jp = 1 + s * step;
         rows(jp, jp + step - 1 <= RW - 2 ? jp + step - 1 : jp);
       }
-      if constexpr (kPre >= n_int) edges_in();
+      if constexpr (kPre >= n_int) edges_in(kFirst);
       if constexpr (RW >= 2) {
         if constexpr (CPL == 2) rows(RW - 1, 0);
-        else { rows(RW - 1, RW - 1); rows(0, 0); }
+        else { rows(RW - 1, RW - 1); if constexpr (kLazy) edges_in(1, false); rows(0, 0); }
       } else {
+        if constexpr (kLazy) edges_in(1, false);
         rows(0, 0);
       }
       if (MODE == kModeFwd) flags |= ((dmax > eps) ? 1u : 0u) << i;
@@ -459,8 +481,8 @@ __global__ void __launch_bounds__(NT) cluster_kernel(ClusterArgs a) {
 
   // Halo exchange in tagged granules (cluster.h): this instance's region of
   // a.gran is [2 parities][S states] x 16 B, of a.sgran [2][H tiles] x 16 B.
-  const __amdgpu_buffer_rsrc_t rg = gran_rsrc(a.gran + (size_t)inst * 4 * S, 32u * (unsigned)S);
-  const __amdgpu_buffer_rsrc_t rs = gran_rsrc(a.sgran + (size_t)inst * 6 * a.H, 48u * (unsigned)a.H);
+  const Gran rg = gran_rsrc(a.gran + (size_t)inst * 4 * S, 32u * (unsigned)S);
+  const Gran rs = gran_rsrc(a.sgran + (size_t)inst * 6 * a.H, 48u * (unsigned)a.H);
   const int ng0 = own0, ng = own0 + (E - own1);  // ghost states: [0, own0) and [own1, E)
   const unsigned salt = (a.salt & 0xFFFu) << 20;  // per call: a stale granule of an earlier call never matches
   // Hand-off store form: write-through (sc1) in general; plain stores (kept in

@@ -85,6 +85,42 @@ __device__ inline double softmax2(double x1, double x2) {
   return hi + log(1.0 + exp(lo - hi));
 }
 
+// ---------------------------------------------------------------------------
+// Device bounds checks (IRLMX_DEVICE_CHECKS=1 builds):
+// IRLMX_DCHECK(cond, bit) records a failed check in this translation unit's
+// device word and lets the caller skip the access instead of faulting the GPU;
+// irlmx_device_check_failures() (capi.hip) syncs the device and returns (and
+// clears) the OR of every translation unit's word.  Off by default: the macro
+// is then constant-true and compiles away.
+// ---------------------------------------------------------------------------
+#ifndef IRLMX_DEVICE_CHECKS
+#define IRLMX_DEVICE_CHECKS 0
+#endif
+constexpr unsigned kCheckIndex = 1;    // ELL row / column slot index outside [0, S)
+constexpr unsigned kCheckGranule = 2;  // granule offset outside its buffer
+constexpr unsigned kCheckTile = 4;     // tile row range / extended tile outside the grid or the LDS buffer
+
+using DcheckTake = unsigned (*)();
+bool register_dcheck(DcheckTake take);  // capi.hip
+
+#if IRLMX_DEVICE_CHECKS
+static __device__ unsigned g_dcheck;
+__device__ inline bool dcheck(bool ok, unsigned bit) {
+  if (!ok) atomicOr(&g_dcheck, bit);
+  return ok;
+}
+static unsigned dcheck_take() {
+  unsigned v = 0, z = 0;
+  if (hipMemcpyFromSymbol(&v, HIP_SYMBOL(g_dcheck), sizeof(v)) != hipSuccess) return ~0u;
+  if (hipMemcpyToSymbol(HIP_SYMBOL(g_dcheck), &z, sizeof(z)) != hipSuccess) return ~0u;
+  return v;
+}
+static const bool g_dcheck_registered = register_dcheck(dcheck_take);
+#define IRLMX_DCHECK(cond, bit) (::irlmx::dcheck((cond), (bit)))
+#else
+#define IRLMX_DCHECK(cond, bit) true
+#endif
+
 // Power-of-two exponent that brings the positive finite m into [0.5, 1).
 __device__ inline int rescale_exponent(double m) {
   if (!(m > 0.0) || !isfinite(m)) return 0;

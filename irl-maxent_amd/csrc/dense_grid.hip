@@ -182,7 +182,7 @@ __device__ inline int dg_plain(const DenseGridArgs& a, int b, int blk, unsigned 
                                unsigned long long* scratch, int* lflag) {
   if (!a.xcd_group) return 0;
   const int tid = threadIdx.x, wave = tid / kWave, lane = tid & (kWave - 1);
-  const __amdgpu_buffer_rsrc_t rx = gran_rsrc(a.xgran + (size_t)b * 2 * a.bpi, 16u * (unsigned)a.bpi);
+  const Gran rx = gran_rsrc(a.xgran + (size_t)b * 2 * a.bpi, 16u * (unsigned)a.bpi);
   unsigned xcc;
   asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
   xcc &= 0xFu;
@@ -257,7 +257,7 @@ __global__ void __launch_bounds__(kDG) dense_grid_kernel(DenseGridArgs a) {
     want |= (c < S ? 1u : 0u) << j;
     cur[j] = (MODE == kModeBwd && c < S && a.term[(size_t)b * S + c]) ? 1.0 : 0.0;  // maxent.py:146-147
   }
-  const __amdgpu_buffer_rsrc_t rg = gran_rsrc(a.gran + (size_t)b * 4 * S, 32u * (unsigned)S);
+  const Gran rg = gran_rsrc(a.gran + (size_t)b * 4 * S, 32u * (unsigned)S);
   const unsigned salt = (a.salt & 0xFFFu) << 20;
   const int pl = dg_plain(a, b, blk, salt, &mred[0][0], &lflag);
   if (pl < 0) {
@@ -461,7 +461,7 @@ __global__ void __launch_bounds__(kDG) dense_bellman_grid_kernel(DenseGridArgs a
     want |= (c < S ? 1u : 0u) << j;
     cur[j] = c < S ? v0 : 0.0;
   }
-  const __amdgpu_buffer_rsrc_t rg = gran_rsrc(a.gran + (size_t)b * 4 * S, 32u * (unsigned)S);
+  const Gran rg = gran_rsrc(a.gran + (size_t)b * 4 * S, 32u * (unsigned)S);
   const unsigned salt = (a.salt & 0xFFFu) << 20;
   const int pl = dg_plain(a, b, blk, salt, &mred[0][0], &lflag);
   if (pl < 0) {

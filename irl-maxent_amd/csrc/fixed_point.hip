@@ -98,7 +98,8 @@ __device__ inline size_t inst_of(const Model& m, int b) { return m.shared ? 0 : 
 // neighbour (row form) of s in slot k
 __device__ inline int row_nbr(const Model& m, int b, int s, int k) {
   if (m.stencil) return stencil_nbr(s, k, m.W, m.H);
-  return m.row_idx[(inst_of(m, b) * m.K + k) * m.S + s];
+  const int t = m.row_idx[(inst_of(m, b) * m.K + k) * m.S + s];
+  return IRLMX_DCHECK(t >= 0 && t < m.S, kCheckIndex) ? t : s;
 }
 
 __device__ inline double row_val(const Model& m, int b, int a, int k, int s) {
@@ -108,7 +109,8 @@ __device__ inline double row_val(const Model& m, int b, int a, int k, int s) {
 // source (column form) of target t in slot k
 __device__ inline int col_src(const Model& m, int b, int t, int k) {
   if (m.stencil) return stencil_nbr(t, k, m.W, m.H);
-  return m.col_idx[(inst_of(m, b) * m.Kc + k) * m.S + t];
+  const int s = m.col_idx[(inst_of(m, b) * m.Kc + k) * m.S + t];
+  return IRLMX_DCHECK(s >= 0 && s < m.S, kCheckIndex) ? s : t;
 }
 
 // ---------------------------------------------------------------------------
@@ -714,6 +716,76 @@ __device__ __forceinline__ void bellman_fused_body(const SoftArgs& a, unsigned c
   }
 }
 
+// Soft VI / VI in numpy's floating-point order (irlmx_soft_backward /
+// irlmx_value_iteration with IRLMX_NUMPY_ORDER): every p[a].dot(v) as
+// np_row_dot sums it, then the per-sweep kernel's statements.  VI has no
+// transcendental function, so its values are bit-identical to the reference's
+// on a Haswell-family host; soft VI's exp / log are ocml's (numpy's SIMD exp /
+// log may differ in the last bit), its dot products follow numpy's order.
+template <bool SOFT, int LAYOUT>
+__global__ void __launch_bounds__(1024) bellman_numpy_order_kernel(SoftArgs a) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  const Model& m = a.m;
+  const int S = m.S, A = m.A;
+  const int b = blockIdx.x, tid = threadIdx.x, nt = blockDim.x;
+  double* buf[2] = {(double*)smem, (double*)smem + S};
+  unsigned long long* slot = (unsigned long long*)(buf[1] + S);
+  const double v0 = SOFT ? -1e200 : 0.0;  // maxent.py:323 / solver.py:29
+  const double* rw = a.reward + (size_t)b * S;
+  for (int s = tid; s < S; s += nt) buf[0][s] = v0;
+  if (tid < 3) slot[tid] = 0ull;
+  __syncthreads();
+  long long it = 0;
+  int r3 = 0;
+  double delta = 0.0;
+  for (;;) {
+    const double* vin = buf[it & 1];
+    double* vout = buf[(it & 1) ^ 1];
+    unsigned long long mx = 0ull;
+    for (int s = tid; s < S; s += nt) {
+      const double r = rw[s];
+      double v = SOFT ? a.phi[(size_t)b * S + s] : 0.0;
+      for (int act = 0; act < A; ++act) {
+        const double dot = np_row_dot<LAYOUT>(m, b, act, s, vin);
+        if (SOFT) {
+          v = softmax2(v, __dadd_rn(r, __dmul_rn(a.discount, dot)));  // maxent.py:329-333
+        } else {
+          const double q = __dmul_rn(a.discount, dot);  // solver.py:44
+          if (a.average) v = act == 0 ? q : __dadd_rn(v, q);
+          else v = act == 0 ? q : ((v != v || q <= v) ? v : q);
+        }
+      }
+      if (!SOFT) v = __dadd_rn(r, a.average ? v / (double)A : v);  // solver.py:47 / :99
+      vout[s] = v;
+      const unsigned long long d = abs_bits(v - vin[s]);
+      mx = d > mx ? d : mx;
+    }
+    mx = wave_max_u64(mx);
+    if ((tid & (kWave - 1)) == 0 && mx) atomicMax(&slot[r3], mx);
+    if (tid == 0) slot[r3 == 2 ? 0 : r3 + 1] = 0ull;
+    __syncthreads();
+    delta = bits_double(slot[r3]);
+    r3 = r3 == 2 ? 0 : r3 + 1;
+    ++it;
+    if (!(delta > a.eps)) break;
+    if (a.max_iter > 0 && it >= a.max_iter) break;
+  }
+  const double* vold = buf[(it & 1) ^ 1];  // input of the last sweep
+  const double* vnew = buf[it & 1];
+  for (int s = tid; s < S; s += nt) {
+    if (a.value) a.value[(size_t)b * S + s] = vnew[s];
+    if (SOFT)
+      for (int act = 0; act < A; ++act) {
+        const double q = __dadd_rn(rw[s], __dmul_rn(a.discount, np_row_dot<LAYOUT>(m, b, act, s, vold)));
+        a.pi[((size_t)b * S + s) * A + act] = exp(q - vnew[s]);  // maxent.py:341
+      }
+  }
+  if (tid == 0) {
+    if (a.iters) a.iters[b] = it;
+    a.status[b] = finish_status(delta, a.eps);
+  }
+}
+
 template <int SPT, int KMAX>
 __global__ void __launch_bounds__(1024) soft_fused_kernel(SoftArgs a) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
@@ -987,8 +1059,8 @@ __global__ void __launch_bounds__(kGridThreads) bellman_grid_kernel(SoftArgs a, 
     }
   }
   if (tid == 0) lflag = 0;
-  const __amdgpu_buffer_rsrc_t rg = gran_rsrc(g.gran + (size_t)b * 6 * S, 48u * (unsigned)S);
-  const __amdgpu_buffer_rsrc_t rd = gran_rsrc(g.dgran + (size_t)b * 8 * g.bpi, 64u * (unsigned)g.bpi);
+  const Gran rg = gran_rsrc(g.gran + (size_t)b * 6 * S, 48u * (unsigned)S);
+  const Gran rd = gran_rsrc(g.dgran + (size_t)b * 8 * g.bpi, 64u * (unsigned)g.bpi);
   const unsigned salt = (g.salt & 0xFFFu) << 20;
   // hand-off store form: write-through (sc1) in general; plain stores (kept in the
   // XCD's L2, where the readers' sc1 loads are served) when every workgroup of
@@ -1184,8 +1256,8 @@ __global__ void __launch_bounds__(kGridThreads) linear_grid_kernel(LinearGridArg
     }
   }
   if (tid == 0) lflag = 0;
-  const __amdgpu_buffer_rsrc_t rg = gran_rsrc(g.gran + (size_t)b * 6 * S, 48u * (unsigned)S);
-  const __amdgpu_buffer_rsrc_t rd = gran_rsrc(g.dgran + (size_t)b * 8 * g.bpi, 64u * (unsigned)g.bpi);
+  const Gran rg = gran_rsrc(g.gran + (size_t)b * 6 * S, 48u * (unsigned)S);
+  const Gran rd = gran_rsrc(g.dgran + (size_t)b * 8 * g.bpi, 64u * (unsigned)g.bpi);
   const unsigned salt = (g.salt & 0xFFFu) << 20;
   bool plain = false;
   {  // XCC ids (bellman_grid_kernel)
@@ -2108,6 +2180,52 @@ extern "C" int irlmx_value_iteration(const irlmx_mdp* mdp, const double* reward,
                                      int32_t* status, void* workspace, size_t workspace_bytes, void* stream) {
   return bellman_common(mdp, reward, nullptr, discount, eps, max_iter, average, nullptr, value, iterations,
                         status, workspace, workspace_bytes, stream, false);
+}
+
+// Soft VI / VI in numpy's order: one workgroup per instance (S <= 4096, S % 4 in {0, 1}).
+static int bellman_numpy_order(const irlmx_mdp* mdp, const double* reward, const double* phi, double discount,
+                               double eps, int64_t max_iter, int average, double* p_action, double* value,
+                               int64_t* iterations, int32_t* status, void* stream, bool soft) {
+  if (int rc = validate(mdp)) return rc;
+  const Model m = make_model(mdp);
+  const char* fn = soft ? "soft_backward_numpy_order" : "value_iteration_numpy_order";
+  if (int rc = need_all(fn, {{reward, "reward"}, {phi, soft ? "terminal_reward" : nullptr},
+                             {p_action, soft ? "p_action" : nullptr}, {value, soft ? nullptr : "value"},
+                             {iterations, "iterations"}, {status, "status"}}))
+    return rc;
+  if (m.S > kFusedMaxStates || (m.S & 3) > 1) {
+    set_error("%s: numpy's order is restated for S <= %d with S %% 4 in {0, 1}, got S=%d", fn, kFusedMaxStates, m.S);
+    return IRLMX_EINVAL;
+  }
+  SoftArgs a{m, reward, phi, discount, eps, (long long)max_iter, average, p_action, value, iterations, status};
+  void (*k)(SoftArgs) = nullptr;
+  if (m.stencil) k = soft ? bellman_numpy_order_kernel<true, IRLMX_LAYOUT_STENCIL5>
+                          : bellman_numpy_order_kernel<false, IRLMX_LAYOUT_STENCIL5>;
+  else if (m.dense) k = soft ? bellman_numpy_order_kernel<true, IRLMX_LAYOUT_DENSE>
+                             : bellman_numpy_order_kernel<false, IRLMX_LAYOUT_DENSE>;
+  else k = soft ? bellman_numpy_order_kernel<true, IRLMX_LAYOUT_ELL> : bellman_numpy_order_kernel<false, IRLMX_LAYOUT_ELL>;
+  const size_t lds = 2 * (size_t)m.S * sizeof(double) + 4 * sizeof(unsigned long long);
+  hipError_t e = hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+  if (e != hipSuccess) return hip_fail(e, "hipFuncSetAttribute");
+  hipLaunchKernelGGL(k, dim3(m.B), dim3(m.S >= 1024 ? 1024 : ((m.S + kWave - 1) / kWave) * kWave), lds,
+                     (hipStream_t)stream, a);
+  e = hipGetLastError();
+  return e == hipSuccess ? 0 : hip_fail(e, fn);
+}
+
+extern "C" int irlmx_soft_backward_numpy_order(const irlmx_mdp* mdp, const double* reward,
+                                               const double* terminal_reward, double discount, double eps,
+                                               int64_t max_iter, double* p_action, double* value,
+                                               int64_t* iterations, int32_t* status, void* stream) {
+  return bellman_numpy_order(mdp, reward, terminal_reward, discount, eps, max_iter, 0, p_action, value, iterations,
+                             status, stream, true);
+}
+
+extern "C" int irlmx_value_iteration_numpy_order(const irlmx_mdp* mdp, const double* reward, double discount,
+                                                 double eps, int32_t average, int64_t max_iter, double* value,
+                                                 int64_t* iterations, int32_t* status, void* stream) {
+  return bellman_numpy_order(mdp, reward, nullptr, discount, eps, max_iter, average, nullptr, value, iterations,
+                             status, stream, false);
 }
 
 extern "C" int irlmx_dense_gemm(const double* m, const double* z, double* c, int32_t rows, int32_t n, int32_t batch,

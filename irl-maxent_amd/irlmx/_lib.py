@@ -68,10 +68,14 @@ SIGNATURES = {
     "irlmx_last_error": (ctypes.c_char_p, []),
     "irlmx_counters": (ctypes.c_int, [_P, _I32]),
     "irlmx_workspace_bytes": (_SZ, [_MDP, _I32]),
+    "irlmx_device_checks_enabled": (ctypes.c_int, []),
+    "irlmx_device_check_failures": (_I64, []),
     "irlmx_backward_maxent": (ctypes.c_int, [_MDP, _P, _P, _I32, _P, _P, _P, _SZ, _P]),
     "irlmx_backward_maxent_numpy_order": (ctypes.c_int, [_MDP, _P, _P, _P, _P, _P]),
     "irlmx_forward_svf": (ctypes.c_int, [_MDP, _P, _P, _P, _D, _I64, _P, _P, _P, _P, _SZ, _P]),
     "irlmx_soft_backward": (ctypes.c_int, [_MDP, _P, _P, _D, _D, _I64, _P, _P, _P, _P, _P, _SZ, _P]),
+    "irlmx_soft_backward_numpy_order": (ctypes.c_int, [_MDP, _P, _P, _D, _D, _I64, _P, _P, _P, _P, _P]),
+    "irlmx_value_iteration_numpy_order": (ctypes.c_int, [_MDP, _P, _D, _D, _I32, _I64, _P, _P, _P, _P]),
     "irlmx_value_iteration": (ctypes.c_int, [_MDP, _P, _D, _D, _I32, _I64, _P, _P, _P, _P, _SZ, _P]),
     "irlmx_execution_plan": (ctypes.c_int, [_MDP, _I32, _P]),
     "irlmx_optimal_policy": (ctypes.c_int, [_P, _I32, _I32, _I32, _P, _P, _P]),

@@ -58,6 +58,16 @@ def counters():
     return dict(zip(_lib.COUNTER_NAMES, [int(v) for v in buf]))
 
 
+def device_check_failures():
+    """Bits of the in-kernel bounds checks that failed since the last call
+    (irlmx_device_check_failures: 1 index, 2 granule, 4 tile); always 0 unless
+    the library is the IRLMX_DEVICE_CHECKS build (libirlmx_checks.so)."""
+    v = int(_lib.load().irlmx_device_check_failures())
+    if v < 0:
+        raise RuntimeError("irlmx_device_check_failures: HIP error")
+    return v
+
+
 def _f64(x, mdp, shape):
     t = torch.as_tensor(x, dtype=torch.float64, device=mdp.device)
     return t.reshape(shape).contiguous()
@@ -133,10 +143,12 @@ def forward_svf(mdp, p_initial, terminal, p_action, eps=1e-5, max_iter=0):
     return svf, iters, status
 
 
-def soft_backward(mdp, reward, terminal_reward, discount, eps=1e-5, max_iter=0):
+def soft_backward(mdp, reward, terminal_reward, discount, eps=1e-5, max_iter=0, numpy_order=False):
     """MaxCausalEnt soft value iteration (maxent.py:279-341).
 
     Returns ``(p_action [B, S, A], value [B, S], iterations [B], status [B])``.
+    ``numpy_order``: every P_a . v summed in numpy's order
+    (irlmx_soft_backward_numpy_order; numpy_order_supported(mdp) models only).
     """
     lib = _lib.load()
     B, S, A = mdp.batch, mdp.n_states, mdp.n_actions
@@ -146,6 +158,12 @@ def soft_backward(mdp, reward, terminal_reward, discount, eps=1e-5, max_iter=0):
     v = torch.empty((B, S), dtype=torch.float64, device=mdp.device)
     iters = torch.empty(B, dtype=torch.int64, device=mdp.device)
     status = torch.empty(B, dtype=torch.int32, device=mdp.device)
+    if numpy_order:
+        _lib.check(lib.irlmx_soft_backward_numpy_order(mdp.struct(), _lib.ptr(r), _lib.ptr(phi), float(discount),
+                                                       float(eps), int(max_iter), _lib.ptr(pi), _lib.ptr(v),
+                                                       _lib.ptr(iters), _lib.ptr(status), _lib.stream_ptr(mdp.device)),
+                   "soft_backward_numpy_order")
+        return pi, v, iters, status
     ws, n = _workspace(mdp, _lib.OP_SOFT_BACKWARD)
     _lib.check(lib.irlmx_soft_backward(mdp.struct(), _lib.ptr(r), _lib.ptr(phi), float(discount), float(eps),
                                        int(max_iter), _lib.ptr(pi), _lib.ptr(v), _lib.ptr(iters),
@@ -154,10 +172,12 @@ def soft_backward(mdp, reward, terminal_reward, discount, eps=1e-5, max_iter=0):
     return pi, v, iters, status
 
 
-def value_iteration(mdp, reward, discount, eps=1e-3, average=False, max_iter=0):
+def value_iteration(mdp, reward, discount, eps=1e-3, average=False, max_iter=0, numpy_order=False):
     """Hard-max (solver.py:9-52) or action-average (solver.py:55-104) value iteration.
 
-    Returns ``(value [B, S], iterations [B], status [B])``.
+    Returns ``(value [B, S], iterations [B], status [B])``.  ``numpy_order``:
+    numpy's summation order (irlmx_value_iteration_numpy_order), values
+    bit-identical to the reference's on a Haswell-family OpenBLAS host.
     """
     lib = _lib.load()
     B, S = mdp.batch, mdp.n_states
@@ -165,6 +185,12 @@ def value_iteration(mdp, reward, discount, eps=1e-3, average=False, max_iter=0):
     v = torch.empty((B, S), dtype=torch.float64, device=mdp.device)
     iters = torch.empty(B, dtype=torch.int64, device=mdp.device)
     status = torch.empty(B, dtype=torch.int32, device=mdp.device)
+    if numpy_order:
+        _lib.check(lib.irlmx_value_iteration_numpy_order(mdp.struct(), _lib.ptr(r), float(discount), float(eps),
+                                                         1 if average else 0, int(max_iter), _lib.ptr(v),
+                                                         _lib.ptr(iters), _lib.ptr(status),
+                                                         _lib.stream_ptr(mdp.device)), "value_iteration_numpy_order")
+        return v, iters, status
     ws, n = _workspace(mdp, _lib.OP_VALUE_ITERATION)
     _lib.check(lib.irlmx_value_iteration(mdp.struct(), _lib.ptr(r), float(discount), float(eps),
                                          1 if average else 0, int(max_iter), _lib.ptr(v), _lib.ptr(iters),

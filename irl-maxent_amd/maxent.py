@@ -7,11 +7,12 @@ GPU through libirlmx.so (``irlmx.ops``); only the demonstration statistics,
 the feature products and the user's optimizer stay on the host, as in the
 reference's outer loop.
 
-The non-causal backward pass (local_action_probabilities and the backward
-half of compute_expected_svf / irl) runs in numpy's own floating-point order
-when the model allows it (S <= 4096 and S % 4 in {0, 1}: every square grid),
-so its policy is bit-identical to the reference's on a Haswell-family
-OpenBLAS host (ops.backward_maxent_numpy_order).
+The backward passes run in numpy's own floating-point order when the model
+allows it (S <= 4096 and S % 4 in {0, 1}: every square grid): the non-causal
+policy (local_action_probabilities, and the backward half of
+compute_expected_svf / irl) is then bit-identical to the reference's on a
+Haswell-family OpenBLAS host, and the soft VI's dot products follow numpy's
+order (ops.*_numpy_order; IRLMX_NUMPY_ORDER=0 turns it off).
 
 Deliberate differences (documented in DESIGN.md):
 * Where the reference's backward pass overflows to NaN (about 13x13 at unit
@@ -102,11 +103,18 @@ def expected_svf_from_policy(p_transition, p_initial, terminal, p_action, eps=1e
     return _host(svf)
 
 
+def _np_order(mdp):
+    """numpy's own summation order for this call (one instance, a model the
+    numpy-order kernels cover; IRLMX_NUMPY_ORDER=0 turns it off)."""
+    return (mdp.batch == 1 and ops.numpy_order_supported(mdp)
+            and os.environ.get("IRLMX_NUMPY_ORDER", "1") != "0")
+
+
 def _backward(mdp, reward, term):
     """The backward policy on the device: numpy's order where the model allows it
     (bit-identical to the reference), the rescaled pass where that overflows."""
     reward = np.asarray(reward.cpu().numpy() if torch.is_tensor(reward) else reward, dtype=np.float64)
-    if mdp.batch == 1 and ops.numpy_order_supported(mdp):
+    if _np_order(mdp):
         pi = ops.backward_maxent_numpy_order(mdp, np.exp(reward), term)   # er = np.exp(reward), maxent.py:142
         if not _rescale() or bool(torch.isfinite(pi).all()):
             return pi
@@ -193,7 +201,7 @@ def local_causal_action_probabilities(p_transition, terminal, reward, discount, 
     """Soft value iteration of MaxCausalEnt IRL; returns exp(Q - V) (maxent.py:279-341)."""
     mdp = _model(p_transition)
     phi = _terminal_reward(terminal, mdp.n_states)
-    pi, _, _, _ = ops.soft_backward(mdp, reward, phi, discount, eps)
+    pi, _, _, _ = ops.soft_backward(mdp, reward, phi, discount, eps, numpy_order=_np_order(mdp))
     return _host(pi)
 
 
@@ -202,7 +210,7 @@ def compute_expected_causal_svf(p_transition, p_initial, terminal, reward, disco
     """Soft value iteration then forward pass (maxent.py:344-380)."""
     mdp = _model(p_transition)
     phi = _terminal_reward(terminal, mdp.n_states)
-    pi, _, _, _ = ops.soft_backward(mdp, reward, phi, discount, eps_lap)
+    pi, _, _, _ = ops.soft_backward(mdp, reward, phi, discount, eps_lap, numpy_order=_np_order(mdp))
     term = ops.terminal_mask(terminal, mdp.n_states, device=mdp.device)
     svf, _, _ = ops.forward_svf(mdp, p_initial, term, pi, eps_svf)
     return _host(svf)
@@ -215,7 +223,7 @@ def irl_causal(p_transition, features, terminal, trajectories, optim, init, disc
     phi = torch.as_tensor(_terminal_reward(terminal, mdp.n_states), device=mdp.device)
 
     def svf_fn(m, reward, term, p0):
-        pi, _, _, _ = ops.soft_backward(m, reward, phi, discount, eps_lap)
+        pi, _, _, _ = ops.soft_backward(m, reward, phi, discount, eps_lap, numpy_order=_np_order(m))
         svf, _, _ = ops.forward_svf(m, p0, term, pi, eps_svf)
         return _host(svf)
 

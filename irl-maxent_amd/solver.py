@@ -1,9 +1,12 @@
 """MI355X drop-in for the reference module ``solver`` (narendasan/irl-maxent, src/solver.py).
 
-Value iteration runs as a device fixed-point loop (irlmx.ops.value_iteration);
+Value iteration runs as a device fixed-point loop (irlmx.ops.value_iteration),
+in numpy's summation order where the model allows it (bit-identical values);
 policy extraction gathers the intended successors' values on the device.
 Names, signatures, defaults and float64 numpy results follow the reference.
 """
+
+import os
 
 import numpy as np
 import torch
@@ -18,17 +21,23 @@ def _model(p):
     return p if isinstance(p, DeviceMDP) else DeviceMDP.resident(p)
 
 
+def _np_order(mdp):
+    # numpy's summation order where the kernels cover the model: values bit-identical
+    # to the reference's (ops.value_iteration numpy_order; IRLMX_NUMPY_ORDER=0 turns it off)
+    return mdp.batch == 1 and ops.numpy_order_supported(mdp) and os.environ.get("IRLMX_NUMPY_ORDER", "1") != "0"
+
+
 def value_iteration(p, reward, discount, eps=1e-3):
     """v <- r + max_a discount * P_a v until max|dv| <= eps (solver.py:9-52)."""
     mdp = _model(p)
-    v, _, _ = ops.value_iteration(mdp, reward, discount, eps, average=False)
+    v, _, _ = ops.value_iteration(mdp, reward, discount, eps, average=False, numpy_order=_np_order(mdp))
     return v[0].cpu().numpy()
 
 
 def stochastic_value_iteration(p, reward, discount, eps=1e-3):
     """As value_iteration with the mean over actions instead of the max (solver.py:55-104)."""
     mdp = _model(p)
-    v, _, _ = ops.value_iteration(mdp, reward, discount, eps, average=True)
+    v, _, _ = ops.value_iteration(mdp, reward, discount, eps, average=True, numpy_order=_np_order(mdp))
     return v[0].cpu().numpy()
 
 

@@ -96,3 +96,50 @@ int blas_order_backward_maxent(const double* P, int S, int A, const uint8_t* ter
   free(pa); free(zs); free(dot); free(za);
   return 0;
 }
+
+/*
+ * value_iteration / stochastic_value_iteration (solver.py:9-52, 55-104) in that
+ * order: q_a = discount * (p[a] @ v) (np.matrix @ 1-d: the same dgemv), then
+ * v = reward + max_a q_a (exact; NaN propagates as np.max does) or
+ * reward + ((q_0 + q_1) + ...) / A (np.average over axis 0), until
+ * max|v_old - v| <= eps.  P [S][S][A] C order; returns the sweep count (or < 0).
+ */
+long long blas_order_value_iteration(const double* P, int S, int A, const double* reward, double discount,
+                                     double eps, int average, long long max_iter, double* v) {
+  if (S <= 0 || A <= 0 || (S & 3) > 1) return -1;
+  double* pa = malloc((size_t)A * S * S * sizeof(double));
+  double* q = malloc((size_t)A * S * sizeof(double));
+  double* vo = malloc((size_t)S * sizeof(double));
+  if (!pa || !q || !vo) {
+    free(pa); free(q); free(vo);
+    return -2;
+  }
+  for (int a = 0; a < A; ++a)
+    for (int s = 0; s < S; ++s)
+      for (int t = 0; t < S; ++t) pa[((size_t)a * S + s) * S + t] = P[((size_t)s * S + t) * A + a];
+  for (int s = 0; s < S; ++s) v[s] = 0.0;  /* solver.py:29 */
+  long long it = 0;
+  double delta = INFINITY;
+  while (delta > eps && (max_iter <= 0 || it < max_iter)) {
+    for (int s = 0; s < S; ++s) vo[s] = v[s];
+    for (int a = 0; a < A; ++a) {
+      blas_order_dgemv_rows(pa + (size_t)a * S * S, S, vo, q + (size_t)a * S);
+      for (int s = 0; s < S; ++s) q[(size_t)a * S + s] = discount * q[(size_t)a * S + s];
+    }
+    delta = 0.0;
+    for (int s = 0; s < S; ++s) {
+      double m = q[s];
+      for (int a = 1; a < A; ++a) {
+        const double x = q[(size_t)a * S + s];
+        if (average) m = m + x;
+        else if (m == m && (x != x || x > m)) m = x;  /* np.max: NaN wins */
+      }
+      v[s] = reward[s] + (average ? m / (double)A : m);
+      const double d = fabs(vo[s] - v[s]);
+      if (d != d || d > delta) delta = d != d ? NAN : (delta != delta ? delta : d);
+    }
+    ++it;
+  }
+  free(pa); free(q); free(vo);
+  return it;
+}

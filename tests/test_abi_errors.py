@@ -76,13 +76,26 @@ def _bwd_np(lib, m, a):
     return lib.irlmx_backward_maxent_numpy_order(m, a["exp_reward"], a["terminal"], a["p_action"], a["status"], NULL)
 
 
+def _soft_np(lib, m, a):
+    return lib.irlmx_soft_backward_numpy_order(m, a["reward"], a["terminal_reward"], 0.7, 1e-5, 0, a["p_action"],
+                                               a["value"], a["iterations"], a["status"], NULL)
+
+
+def _vi_np(lib, m, a):
+    return lib.irlmx_value_iteration_numpy_order(m, a["reward"], 0.9, 1e-3, 0, 0, a["value"], a["iterations"],
+                                                 a["status"], NULL)
+
+
 ENTRY = {
     "backward_maxent": (1, _bwd, ("reward", "terminal", "p_action", "status")),
     "backward_maxent_numpy_order": (1, _bwd_np, ("exp_reward", "terminal", "p_action", "status")),
     "forward_svf": (2, _fwd, ("p_initial", "terminal", "p_action", "svf", "iterations", "status")),
     "soft_backward": (3, _soft, ("reward", "terminal_reward", "p_action", "iterations", "status")),
     "value_iteration": (4, _vi, ("reward", "value", "iterations", "status")),
+    "soft_backward_numpy_order": (3, _soft_np, ("reward", "terminal_reward", "p_action", "iterations", "status")),
+    "value_iteration_numpy_order": (4, _vi_np, ("reward", "value", "iterations", "status")),
 }
+NO_WORKSPACE = {"backward_maxent_numpy_order", "soft_backward_numpy_order", "value_iteration_numpy_order"}
 ARGS = ("reward", "terminal", "p_action", "status", "p_initial", "svf", "iterations", "terminal_reward", "value",
         "exp_reward")
 
@@ -153,7 +166,7 @@ def test_optional_arrays_accepted_as_null(lib):
     assert _soft(lib, ctypes.byref(m), a) == EWORKSPACE
 
 
-@pytest.mark.parametrize("fn", sorted(set(ENTRY) - {"backward_maxent_numpy_order"}))  # (takes no workspace)
+@pytest.mark.parametrize("fn", sorted(set(ENTRY) - NO_WORKSPACE))
 @pytest.mark.parametrize("layout", ["stencil", "ell", "dense"])
 def test_workspace_too_small(lib, fn, layout):
     op, call, _ = ENTRY[fn]
@@ -253,6 +266,7 @@ def test_numpy_order_sizes_einval(lib, S, W, H):
     """numpy's order is restated for S <= 4096 with S % 4 in {0, 1} only
     (oracle/blas_order.c): other sizes are rejected, not approximated."""
     m = model(S=S, W=W, H=H)
-    a = args_for(lib, model(), 1)
-    assert _bwd_np(lib, ctypes.byref(m), a) == EINVAL
-    assert "numpy's order is restated for S <= 4096" in err(lib), err(lib)
+    for call, op in ((_bwd_np, 1), (_soft_np, 3), (_vi_np, 4)):
+        a = args_for(lib, model(), op)
+        assert call(lib, ctypes.byref(m), a) == EINVAL
+        assert "numpy's order is restated for S <= 4096" in err(lib), err(lib)

@@ -1,4 +1,4 @@
-"""Multi-process paths of the instance sharding (gloo, world sizes 2 and 4).
+"""Multi-process paths of the instance sharding (gloo, world sizes 2, 4 and 8).
 
 CPU: shard ranges cover every instance exactly once; the timing max-reduction
 and the result gather work over gloo.  GPU: two ranks share cuda:0 and each
@@ -91,7 +91,7 @@ BENCH_WORKER = textwrap.dedent("""
     dist.init_process_group("gloo", init_method="tcp://127.0.0.1:{port}", rank={rank}, world_size={world})
     import bench
     from irlmx.shard import instance_slips, max_over_ranks, shard_range
-    rank, world, per_gpu = dist.get_rank(), {world}, 4
+    rank, world, per_gpu = dist.get_rank(), {world}, {per_gpu}
     lo, hi = shard_range(per_gpu * world, world, rank)
     done = []
     def step(i, timed):  # stub: rank 1 is the slow rank
@@ -101,23 +101,27 @@ BENCH_WORKER = textwrap.dedent("""
     emax = max_over_ranks(elapsed)
     value, ms = bench.headline(emax, per_gpu, world, 3)
     json.dump({{"rank": rank, "lo": lo, "hi": hi, "slips": instance_slips(range(lo, hi), per_gpu * world).tolist(),
-               "elapsed": elapsed, "emax": emax, "value": value, "ms": ms, "done": done}},
+               "elapsed": elapsed, "emax": emax, "value": value, "ms": ms, "done": done,
+               "device": bench.rank_device({rank}, 8)}},
               open({out!r} + f".{{rank}}.json", "w"))
     dist.destroy_process_group()
 """)
 
 
-@pytest.mark.parametrize("world", [2, 4])
-def test_bench_timing_over_gloo(tmp_path, world):
-    """bench.py's multi-rank arithmetic with a stubbed step (gloo, 2 and 4 ranks):
+@pytest.mark.parametrize("world,per_gpu", [(2, 4), (4, 4), (8, 32)])
+def test_bench_timing_over_gloo(tmp_path, world, per_gpu):
+    """bench.py's multi-rank arithmetic with a stubbed step (gloo; 2 and 4 ranks,
+    and config 4's layout: 8 ranks x 32 instances = the 256-instance batch):
     each rank times exactly K steps after W warm-ups between barriers, the elapsed
-    time is the max over ranks, value = instances on all ranks x K / that max, and
-    the shards cover the global batch with the bench's per-instance slips."""
+    time is the max over ranks, value = instances on all ranks x K / that max, the
+    shards cover the global batch with the bench's per-instance slips, and every
+    rank of an 8-GPU node gets its own device."""
     import json
     port = _free_port()
     out = str(tmp_path / "bench")
     procs = [subprocess.Popen([sys.executable, "-c", BENCH_WORKER.format(root=ROOT, pkg=PKG_DIR, port=port, rank=r,
-                                                                          out=out, world=world)], cwd=ROOT)
+                                                                          out=out, world=world, per_gpu=per_gpu)],
+                              cwd=ROOT)
              for r in range(world)]
     for p in procs:
         assert p.wait(timeout=240) == 0
@@ -125,10 +129,22 @@ def test_bench_timing_over_gloo(tmp_path, world):
     assert all(r["emax"] == max(x["elapsed"] for x in res) for r in res)
     assert res[-1]["elapsed"] >= 3 * 0.02 * world
     for r in res:
-        assert r["value"] == 4 * world * 3 / r["emax"] and abs(r["ms"] - r["emax"] / 3 * 1e3) < 1e-9
+        assert r["value"] == per_gpu * world * 3 / r["emax"] and abs(r["ms"] - r["emax"] / 3 * 1e3) < 1e-9
         assert r["done"] == [[0, False], [1, True], [2, True], [3, True]]
-    assert [(r["lo"], r["hi"]) for r in res] == [(4 * k, 4 * k + 4) for k in range(world)]
-    assert sum((r["slips"] for r in res), []) == [0.1 + 0.2 * b / (4 * world) for b in range(4 * world)]
+    assert [(r["lo"], r["hi"]) for r in res] == [(per_gpu * k, per_gpu * k + per_gpu) for k in range(world)]
+    B = per_gpu * world
+    assert sum((r["slips"] for r in res), []) == [0.1 + 0.2 * b / B for b in range(B)]
+    assert sorted(r["device"] for r in res) == list(range(world))   # one distinct GPU per rank
+
+
+def test_rank_device_mapping():
+    """bench.py's LOCAL_RANK -> device choice: one GPU per rank on a full node;
+    more ranks than GPUs (a rehearsal on a 1-GPU box) share them round-robin."""
+    import bench
+    assert [bench.rank_device(r, 8) for r in range(8)] == list(range(8))
+    assert [bench.rank_device(r, 1) for r in range(4)] == [0, 0, 0, 0]
+    assert [bench.rank_device(r, 2) for r in range(4)] == [0, 1, 0, 1]
+    assert bench.rank_device(3, 0) == 0
 
 
 def test_gloo_gather_and_max(tmp_path):

@@ -192,8 +192,61 @@ def test_numpy_order_generic_and_batched(dev):
 
 
 def test_causal_policy_argmax(dev):
+    """The drop-in local_causal_action_probabilities sums every P_a . v in numpy's
+    order (irlmx_soft_backward_numpy_order), so the policy's mirror-symmetric
+    ties (diagonal states of the unit-reward cases, decided in the last bit by
+    that order) fall as the reference's do: argmax identical at every pinned
+    case, sweep counts identical, values within 1e-9.  (exp / log are the
+    device's: the reference's own bits change with numpy's SIMD exp / log --
+    NPY_DISABLE_CPU_FEATURES=AVX512F gives other bits, the same argmax.)"""
     import maxent as M
+    from irlmx import DeviceMDP, ops
     for name, P, term, r, g, ref in _pinned_causal_cases():
         pi = M.local_causal_action_probabilities(P, term, r, g)
         got, want = np.argmax(pi, axis=1), np.argmax(ref, axis=1)
         assert np.array_equal(got, want), (name, _argmax_report(got, want))
+        assert np.max(np.abs(pi - ref)) <= 1e-9 * np.max(np.abs(ref)), name
+        _, _, ks_ref = O.soft_backward(P, term, r, g)
+        for layout in ("stencil", "ell", "dense"):
+            mdp = DeviceMDP.from_dense(P, device=dev, layout=layout)
+            p2, _, ks, st = ops.soft_backward(mdp, r, O.terminal_reward(term, P.shape[0]), g, numpy_order=True)
+            assert int(ks[0]) == ks_ref and int(st[0]) == 0, (name, layout)
+            assert torch.equal(p2[0].cpu(), torch.as_tensor(pi)), (name, layout)   # same arithmetic, any layout
+
+
+def test_value_iteration_numpy_order_bit_identical(dev):
+    """solver.value_iteration / stochastic_value_iteration run in numpy's order:
+    values and sweep counts bit-identical to the reference's output for every
+    golden VI case (5x5 / 16x16, max and average, det4, config 1, the non-grid
+    tables on the ELL and DENSE layouts), and to the C restatement
+    (oracle/blas_order.c) at 32x32 and 64x64 with random rewards."""
+    import solver as S
+    from irlmx import DeviceMDP, ops
+    z = load_golden("vi")
+    for c in [str(n) for n in z["names"]]:
+        if c.startswith("det"):
+            continue
+        P = O.icy_gridworld_table(int(z[c + "__size"]), 0.2)
+        fn = S.stochastic_value_iteration if bool(z[c + "__average"]) else S.value_iteration
+        v = fn(P, z[c + "__reward"], float(z[c + "__discount"]))
+        assert np.array_equal(v, z[c + "__value"]), c
+    assert np.array_equal(S.value_iteration(O.gridworld_table(4), z["det4__reward"], 0.5), z["det4__value"])
+    z1 = load_golden("config1")
+    assert np.array_equal(S.value_iteration(z1["p_transition"], z1["reward"], 0.7), z1["value"])
+    g = load_golden("generic")
+    for c in [str(n) for n in g["names"]]:
+        P, r = g[c + "__P"], g[c + "__reward"]
+        for layout in ("ell", "dense"):
+            mdp = DeviceMDP.from_dense(P, device=dev, layout=layout)
+            for avg, key in ((False, "__v"), (True, "__va")):
+                v, k, _ = ops.value_iteration(mdp, r, 0.9, average=avg, numpy_order=True)
+                assert np.array_equal(v[0].cpu().numpy(), g[c + key]), (c, layout, avg)
+    rng = np.random.default_rng(9)
+    for size in (32, 64):
+        P = O.icy_gridworld_table(size, 0.25)
+        r = rng.uniform(-1.0, 1.0, size * size)
+        mdp = DeviceMDP.icy_gridworld(size, 0.25, device=dev)
+        for avg in (False, True):
+            ref, kr = O.value_iteration_blas_order(P, r, 0.95, average=avg)
+            v, k, _ = ops.value_iteration(mdp, r, 0.95, average=avg, numpy_order=True)
+            assert int(k[0]) == kr and np.array_equal(v[0].cpu().numpy(), ref), (size, avg)
