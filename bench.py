@@ -512,7 +512,8 @@ def main(argv=None):
     e_f = np.empty((per_gpu, S))
     p_0 = np.empty((per_gpu, S))
     for i, b in enumerate(ids):
-        e_f[i], p_0[i], _ = demos.sample(rv[i], size, terminal, 0, n=200, seed=1234 + int(b))
+        e_f[i], p_0[i], _ = demos.sample(rv[i], size, terminal, 0, n=200, seed=1234 + int(b),
+                                         max_len=demos.safety_cap(size))
     irl = BatchedMaxEnt(mdp, e_f, p_0, terminal, causal=causal, discount=DISCOUNT if causal else None)
     plans = {"backward": ops.execution_plan(mdp, "soft_backward" if causal else "backward"),
              "forward": ops.execution_plan(mdp, "forward")}

@@ -32,6 +32,14 @@ void count_event(int which) {
   if (which >= 0 && which < IRLMX_COUNTERS_LEN) g_counters[which].fetch_add(1, std::memory_order_relaxed);
 }
 
+void note_exchange_timeout(const char* shape) {
+  static std::atomic<bool> told{false};
+  if (!told.exchange(true))
+    fprintf(stderr,
+            "irlmx: %s shape: an exchange timed out (a workgroup descheduled or a lost granule); the call was rerun "
+            "on the per-sweep shape (counter rerun_timeout; IRLMX_STRICT_EXCHANGE=1 makes it an error)\n", shape);
+}
+
 static std::vector<DcheckTake>& dcheck_registry() {
   static std::vector<DcheckTake> r;
   return r;

@@ -1116,6 +1116,7 @@ int cluster_run(int mode, const ClusterPlan& plan, ClusterArgs a, int B, hipStre
       return IRLMX_EHIP;
     }
     count_event(IRLMX_CTR_RERUN_TIMEOUT);
+    note_exchange_timeout("cluster");
     return kClusterNotResident;
   }
   return (err & 2) ? kClusterNonFinite : 0;

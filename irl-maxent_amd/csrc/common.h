@@ -13,6 +13,10 @@ constexpr int kWave = 64;
 constexpr int kStencilK = 5;  // self, +x, -x, +y, -y
 
 void count_event(int which);  // irlmx_counters (capi.hip): IRLMX_CTR_*
+// An exchange timed out and the call is rerun per sweep (capi.hip): the first
+// time in a process a line on stderr, so a lost or mistagged granule does not
+// pass silently as a slow success (the counter records every one).
+void note_exchange_timeout(const char* shape);
 
 // Direction k of the 5-point stencil, in the reference's action order
 // (gridworld.py:47: (1,0), (-1,0), (0,1), (0,-1)); k = 0 is "stay".

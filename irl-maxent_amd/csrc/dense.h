@@ -129,6 +129,8 @@ struct DenseGridArgs {
   int rb, bpi, nb, xcd_group; // (set by dense_grid_run)
   unsigned salt;
   int n_resident;
+  unsigned long long gather_ticks;  // exchange timeout (kGatherTicks unless a test shortens it)
+  int test_drop;              // tests only (IRLMX_TEST_DROP_TILE): this workgroup leaves after the rendezvous, else -1
 };
 // mode: kModeFwd / kModeBwd (cluster.h).  False when the rows do not fit in
 // registers at one workgroup per CU (IRLMX_DENSE_GRID=0 disables the shape,

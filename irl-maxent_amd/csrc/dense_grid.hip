@@ -190,7 +190,7 @@ __device__ inline int dg_plain(const DenseGridArgs& a, int b, int blk, unsigned 
   if (tid == 0) gran_store(rx, (unsigned)blk * 16u, xcc, htag, false);
   unsigned off[1] = {(unsigned)(tid < a.bpi ? tid : 0) * 16u};
   unsigned long long v[1] = {xcc};
-  if (!gran_gather<1>(rx, rx, off, tid < a.bpi ? 1u : 0u, htag, v)) *lflag = 1;
+  if (!gran_gather<1>(rx, rx, off, tid < a.bpi ? 1u : 0u, htag, v, a.gather_ticks)) *lflag = 1;
   const unsigned long long diff = wave_or_u64(tid < a.bpi ? (v[0] ^ xcc) : 0ull);
   if (lane == 0) scratch[wave] = diff;
   __syncthreads();
@@ -223,6 +223,7 @@ __global__ void __launch_bounds__(kDG) dense_grid_kernel(DenseGridArgs a) {
     if (tid == 0) atomicOr(a.err, kErrNotResident);
     return;
   }
+  if (b * a.bpi + blk == a.test_drop) return;  // tests: a workgroup that stops publishing (exchange-timeout path)
   const int row0 = blk * RB;
   if (MODE == kModeFwd && a.bad[b]) {  // non-finite policy: the reference's dense product is NaN after one sweep
     if (tid < RB && row0 + tid < S) a.out[(size_t)b * S + row0 + tid] = kNaN;
@@ -332,7 +333,7 @@ __global__ void __launch_bounds__(kDG) dense_grid_kernel(DenseGridArgs a) {
 #pragma unroll
       for (int j = 0; j < CPT; ++j) off[j] = (unsigned)(k & 1) * 16u * (unsigned)S + off0[j];
       unsigned long long v[CPT];
-      if (!gran_gather<CPT>(rg, rg, off, want, tag, v)) lflag = 1;
+      if (!gran_gather<CPT>(rg, rg, off, want, tag, v, a.gather_ticks)) lflag = 1;
       unsigned long long d = 0ull;
 #pragma unroll
       for (int j = 0; j < CPT; ++j) {
@@ -428,6 +429,7 @@ __global__ void __launch_bounds__(kDG) dense_bellman_grid_kernel(DenseGridArgs a
     if (tid == 0) atomicOr(a.err, kErrNotResident);
     return;
   }
+  if (b * a.bpi + blk == a.test_drop) return;  // tests: see dense_grid_kernel
   const int row0 = blk * RB;
   const size_t tab = a.shared ? 0 : (size_t)b;
   const double* Pb = a.P + tab * (size_t)A * S * S;
@@ -526,7 +528,7 @@ __global__ void __launch_bounds__(kDG) dense_bellman_grid_kernel(DenseGridArgs a
 #pragma unroll
       for (int j = 0; j < CPT; ++j) off[j] = (unsigned)(k & 1) * 16u * (unsigned)S + off0[j];
       unsigned long long v[CPT];
-      if (!gran_gather<CPT>(rg, rg, off, want, tag, v)) lflag = 1;
+      if (!gran_gather<CPT>(rg, rg, off, want, tag, v, a.gather_ticks)) lflag = 1;
       unsigned long long d = 0ull;
 #pragma unroll
       for (int j = 0; j < CPT; ++j) {
@@ -694,6 +696,11 @@ static int launch_grid(void* fn, const DenseGridPlan& p, DenseGridArgs a, int ro
   a.salt = g_dg_salt.fetch_add(1, std::memory_order_relaxed);
   // (IRLMX_TEST_NOT_RESIDENT=1, tests only: one workgroup more than launched -> the per-sweep rerun)
   a.n_resident = p.bpi * a.B + (env_int("IRLMX_TEST_NOT_RESIDENT", 0) ? 1 : 0);
+  // (IRLMX_TEST_DROP_TILE / IRLMX_TEST_EXCHANGE_TIMEOUT_MS, tests only: one workgroup
+  // leaves after the rendezvous, its neighbours time out -> the per-sweep rerun)
+  a.test_drop = env_int("IRLMX_TEST_DROP_TILE", -1);
+  const int tmo_ms = env_int("IRLMX_TEST_EXCHANGE_TIMEOUT_MS", 0);
+  a.gather_ticks = tmo_ms > 0 ? (unsigned long long)tmo_ms * 100000ull : kGatherTicks;
   const int grid = p.xcd ? 8 * ((a.B + 7) / 8) * p.bpi : p.bpi * a.B;
   void* args[] = {&a};
   hipError_t e = hipLaunchKernel(fn, dim3(grid), dim3(kDG), args, 0, st);
@@ -708,6 +715,7 @@ static int launch_grid(void* fn, const DenseGridPlan& p, DenseGridArgs a, int ro
     set_error("dense grid shape: exchange timed out (workgroups not co-resident?)");
     return IRLMX_EHIP;
   }
+  if (timeout) note_exchange_timeout("dense grid");
   if (err) {  // not all workgroups ran at once, or an exchange timed out: the per-sweep shape
     count_event(timeout ? IRLMX_CTR_RERUN_TIMEOUT : IRLMX_CTR_RERUN_NOT_RESIDENT);
     e = hipMemsetAsync(a.err, 0, 4 * sizeof(int), st);

@@ -1546,6 +1546,7 @@ static int grid_launch(const Model& m, int op, const GridPlan& gp, void** args, 
     set_error("grid shape: exchange timed out (workgroups not co-resident?)");
     return IRLMX_EHIP;
   }
+  if (timeout) note_exchange_timeout("grid");
   if (err) {
     count_event(timeout ? IRLMX_CTR_RERUN_TIMEOUT : IRLMX_CTR_RERUN_NOT_RESIDENT);
     e = hipMemsetAsync(ws.err, 0, 4 * sizeof(int), st);
@@ -1797,6 +1798,7 @@ static int dense_backward(const Model& m, const double* reward, const uint8_t* t
     const int rc = dense_grid_run(kModeBwd, dp, a, st);
     if (rc != kClusterNotResident) return rc;  // else: the per-sweep shape below
   }
+  count_event(IRLMX_CTR_SWEEP_CALLS);
   dense_bwd_init_launch(d, terminal, w, st);
   const long long collapsed = 2LL * m.S - 1;
   const bool gemm = dense_gemm(m);
@@ -1941,6 +1943,7 @@ extern "C" int irlmx_forward_svf(const irlmx_mdp* mdp, const double* p_initial, 
       const int rc = dense_grid_run(kModeFwd, dp, ga, st);
       if (rc != kClusterNotResident) return rc;  // else: the per-sweep shape below
     }
+    count_event(IRLMX_CTR_SWEEP_CALLS);
     int rc = run_until_done(ws, m.B, st, [&](long long it, int r3) {
       dense_fwd_sweep_launch(d, p_initial, eps, (long long)max_iter, status, w, it, r3, st);
     });
@@ -2134,6 +2137,7 @@ static int bellman_common(const irlmx_mdp* mdp, const double* reward, const doub
       if (rc != kClusterNotResident) return rc;  // else: the per-sweep shape below
     }
     hipError_t gerr = hipSuccess;
+    count_event(IRLMX_CTR_SWEEP_CALLS);
     int rc = run_until_done(ws, m.B, st, [&](long long it, int r3) {
       if (gemm) {
         const hipError_t e = dense_bellman_gemm_sweep_launch(d, db, w, it, r3, st);

@@ -9,7 +9,9 @@ once, entirely on the device:
                                               soft VI maxent.py:279-341)
     svf    = forward(p0, pi)                 (maxent.py:63-114, until max|dd| <= eps)
     grad   = e_features - F^T . svf          (maxent.py:248 / 445)
-    theta *= exp(lr_k * grad)                (ExpSga + linear_decay, optimizer.py:154-167, 217-240)
+    theta  = optimizer(theta, grad, k)       (default ExpSga + linear_decay, optimizer.py:154-167,
+                                              217-240; any of irlmx.optim's Sga, ExpSga,
+                                              NormalizeGrad with the reference's schedules)
 
 ``F`` is the identity (``features=None``, the configs' case: reward = theta),
 one ``[S, F]`` matrix shared by all instances, or ``[B, S, F]``.  ``run()``
@@ -26,10 +28,13 @@ CUs per instance) -- so a stopped instance no longer pays its 2*S backward
 sweeps and its forward pass every step.  Per-instance results do not depend on
 the batch they run in (every kernel shape and plan performs the same float64
 operations in the same order per instance), so a compacted run equals an
-uncompacted one bit for bit with identity features
-(tests/test_gpu_full_run.py); with a feature matrix the F . theta / F^T . svf
-products are torch GEMMs whose summation order may change with the batch size
-(rounding-level differences).
+uncompacted one bit for bit with identity features on the STENCIL5 and ELL
+layouts (tests/test_gpu_full_run.py).  Two exceptions change rounding, not
+results beyond it: with a feature matrix the F . theta / F^T . svf products are
+torch GEMMs whose summation order may change with the batch size, and on the
+DENSE layout the planner picks the GEMM or streaming kernel, the GEMM's
+split-K waves and the dense-grid row blocking from the working batch, each with
+its own per-row summation order (tested to 1e-9 against the uncompacted run).
 
 No host round trip happens inside a step except the forward pass's own
 convergence polling on the per-sweep shape.
@@ -40,6 +45,7 @@ import torch
 
 from . import ops
 from .mdp import DeviceMDP
+from .optim import ExpSga, linear_decay
 
 
 def terminal_reward(terminal, n_states, batch=1, device=None):
@@ -56,7 +62,12 @@ def terminal_reward(terminal, n_states, batch=1, device=None):
 
 class BatchedMaxEnt:
     def __init__(self, mdp: DeviceMDP, e_features, p_initial, terminal, features=None, lr0=0.2,
-                 eps_esvf=1e-5, theta0=1.0, rescale=True, causal=False, discount=None, eps_lap=1e-5):
+                 eps_esvf=1e-5, theta0=1.0, rescale=True, causal=False, discount=None, eps_lap=1e-5,
+                 optimizer=None):
+        """``theta0``: a float (the reference's Constant init, optimizer.py:369-398) or
+        an array [F] or [B, F] (e.g. drawn with the reference's Uniform init,
+        optimizer.py:334-366).  ``optimizer``: an irlmx.optim optimiser (default
+        ExpSga(linear_decay(lr0)), the reference main.py's choice)."""
         self.mdp = mdp
         dev = mdp.device
         B, S = mdp.batch, mdp.n_states
@@ -82,8 +93,13 @@ class BatchedMaxEnt:
             self.phi = terminal_reward(terminal, S, batch=B, device=dev)
         self.discount = discount
         self.eps_lap = eps_lap
-        self.theta = torch.full((B, n_f), float(theta0), dtype=torch.float64, device=dev)
+        if np.ndim(theta0) == 0:
+            self.theta = torch.full((B, n_f), float(theta0), dtype=torch.float64, device=dev)
+        else:
+            t0 = torch.as_tensor(np.asarray(theta0, dtype=np.float64), device=dev)
+            self.theta = t0.expand(B, n_f).clone() if t0.dim() == 1 else t0.reshape(B, n_f).clone()
         self.lr0 = lr0
+        self.optimizer = optimizer if optimizer is not None else ExpSga(linear_decay(lr0))
         self.eps_esvf = eps_esvf
         self.rescale = rescale
         self.k = 0
@@ -102,9 +118,6 @@ class BatchedMaxEnt:
     def working_batch(self):
         """Instances the next step computes (all, or the active ones after compact())."""
         return self.batch if self._work is None else int(self._work["idx"].numel())
-
-    def lr(self, k):
-        return self.lr0 / (1.0 + float(k))   # linear_decay(lr0, 1, 1)
 
     # -- working set ----------------------------------------------------------
 
@@ -183,12 +196,12 @@ class BatchedMaxEnt:
         return ops.forward_svf(self._w("mdp"), self._w("p_initial"), self._w("terminal"), pi, self.eps_esvf)
 
     def update(self, svf):
-        """ExpSga step on the working set's theta (optimizer.py:154-167); stopped
-        instances stay frozen.  Returns the gradient [n, F]."""
+        """Optimiser step on the working set's theta (default ExpSga,
+        optimizer.py:154-167); stopped instances stay frozen.  Returns the gradient [n, F]."""
         theta = self._theta_w()
         act = self._active_w()
         grad = self._w("e_features") - self.features_t(svf)
-        new = theta * torch.exp(self.lr(self.k) * grad)
+        new = self.optimizer.apply(theta, grad, self.k)
         delta = torch.where(act, (new - theta).abs().amax(dim=1),
                             torch.zeros((), dtype=torch.float64, device=theta.device))
         new = torch.where(act.unsqueeze(1), new, theta)

@@ -40,6 +40,13 @@ def stencil_targets(size):
                      np.where(y + 1 < size, s + size, -1), np.where(y > 0, s - size, -1)], axis=1)
 
 
+def safety_cap(size):
+    """A step cap for callers that must not hang on a trajectory that can never
+    reach a terminal state (bench.py, the tests): 64 x the grid side, far above
+    any expert trajectory of these worlds (a cut raises by default)."""
+    return 64 * size
+
+
 class TruncatedDemonstrations(ValueError):
     """Some trajectories were cut at ``max_len`` before reaching a terminal state."""
 
@@ -50,7 +57,8 @@ def sample(row_val, size, terminal, start, n=200, seed=0, beta=2.0, max_len=None
 
     Like the reference (trajectory.py:76, ``while not terminal``) a trajectory
     runs until it reaches a terminal state: with ``max_len=None`` there is no
-    cap.  With a cap, trajectories still alive after ``max_len`` steps are cut
+    cap, so the caller must guarantee that terminals are reachable (bench.py
+    and the tests pass ``max_len=safety_cap(size)``).  With a cap, trajectories still alive after ``max_len`` steps are cut
     (their last state then counts as a final state, which skews the feature
     expectation): ``on_truncate="raise"`` raises TruncatedDemonstrations,
     ``"allow"`` keeps them.  Returns ``(e_features, p_initial, lengths)`` for

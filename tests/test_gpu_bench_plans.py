@@ -82,7 +82,8 @@ def run_bench_workload(dev, cfg, size, per_gpu, n_steps, causal=False):
         assert float(slips[b]) == float(z[f"{b}__slip"])
         e_f[b], p0[b] = z[f"{b}__e_f"], z[f"{b}__p0"]
     b = checked[0]
-    ef_dev, p0_dev, _ = demos.sample(mdp.row_val[b].cpu().numpy(), size, [S - 1], 0, n=200, seed=1234 + b)
+    ef_dev, p0_dev, _ = demos.sample(mdp.row_val[b].cpu().numpy(), size, [S - 1], 0, n=200, seed=1234 + b,
+                                     max_len=demos.safety_cap(size))
     assert np.array_equal(ef_dev, z[f"{b}__e_f"]) and np.array_equal(p0_dev, z[f"{b}__p0"])
     irl = BatchedMaxEnt(mdp, e_f, p0, [S - 1], causal=causal, discount=0.7 if causal else None)
     steps = []
@@ -196,7 +197,7 @@ def test_config3_timed_steps_plan_independent(dev):
     e_f = np.empty((B, S))
     p0 = np.empty((B, S))
     for b in range(B):
-        e_f[b], p0[b], _ = demos.sample(rv[b], size, [S - 1], 0, n=200, seed=1234 + b)
+        e_f[b], p0[b], _ = demos.sample(rv[b], size, [S - 1], 0, n=200, seed=1234 + b, max_len=demos.safety_cap(size))
     pick = np.array([0, 63])
     sub = mdp.take(pick)
     assert plan_subset(ops.execution_plan(mdp, "backward"), C3_BWD_PLAN) == C3_BWD_PLAN
@@ -229,7 +230,7 @@ def test_config4_full_vectors_plan_independent(dev):
     e_f = np.empty((B, S))
     p0 = np.empty((B, S))
     for b in range(B):
-        e_f[b], p0[b], _ = demos.sample(rv[b], size, [S - 1], 0, n=200, seed=1234 + b)
+        e_f[b], p0[b], _ = demos.sample(rv[b], size, [S - 1], 0, n=200, seed=1234 + b, max_len=demos.safety_cap(size))
     pick = np.array([0, 31])
     sub = mdp.take(pick)
     assert plan_subset(ops.execution_plan(mdp, "backward"), C4_BWD_PLAN) == C4_BWD_PLAN

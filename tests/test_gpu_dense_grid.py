@@ -253,6 +253,7 @@ def test_dense_grid_not_resident_rerun(dev, monkeypatch):
     monkeypatch.delenv("IRLMX_TEST_NOT_RESIDENT")
     after = ops.counters()
     assert after["rerun_not_resident"] == before["rerun_not_resident"] + 1
+    assert after["sweep_calls"] == before["sweep_calls"] + 1   # the per-sweep rerun is counted
     assert torch.equal(got, ref)
     # soft VI likewise
     from irlmx.batch import terminal_reward
@@ -265,9 +266,52 @@ def test_dense_grid_not_resident_rerun(dev, monkeypatch):
     monkeypatch.setenv("IRLMX_TEST_NOT_RESIDENT", "1")
     got = ops.soft_backward(mdp, r, phi, 0.7)
     monkeypatch.delenv("IRLMX_TEST_NOT_RESIDENT")
-    assert ops.counters()["rerun_not_resident"] == before["rerun_not_resident"] + 1
+    after = ops.counters()
+    assert after["rerun_not_resident"] == before["rerun_not_resident"] + 1
+    assert after["sweep_calls"] == before["sweep_calls"] + 1
     for x, y in zip(got, ref):
         assert torch.equal(x, y)
+
+
+def test_dense_grid_exchange_timeout_rerun(dev, monkeypatch):
+    """One workgroup of a dense-grid launch leaves right after the rendezvous
+    (IRLMX_TEST_DROP_TILE) and the others' all-gather times out
+    (IRLMX_TEST_EXCHANGE_TIMEOUT_MS): the forward, the backward and soft VI
+    rerun on the per-sweep dense shape with its results, counted as
+    rerun_timeout and sweep_calls; IRLMX_STRICT_EXCHANGE=1 reports it instead."""
+    from irlmx import _lib, ops
+    from irlmx.batch import terminal_reward
+    n = 400
+    mdp, _ = dense_model(dev, n, 4, 2, True, seed=11)
+    r = np.random.default_rng(1).uniform(0.0, 1.0, (2, n))
+    tm = ops.terminal_mask([n - 1], n, batch=2, device=dev)
+    phi = terminal_reward([n - 1], n, 2, dev)
+    p0 = np.zeros((2, n))
+    p0[:, 0] = 1.0
+    pi = ops.backward_maxent(mdp, r, tm)
+    calls = {"backward": lambda: ops.backward_maxent(mdp, r, tm),
+             "forward": lambda: ops.forward_svf(mdp, p0, tm, pi, max_iter=500),
+             "soft_backward": lambda: ops.soft_backward(mdp, r, phi, 0.7)}
+    for op, run in calls.items():
+        assert ops.execution_plan(mdp, op)["shape"] == "dense-grid", op
+        monkeypatch.setenv("IRLMX_DENSE_GRID", "0")
+        ref = run()
+        monkeypatch.delenv("IRLMX_DENSE_GRID")
+        before = ops.counters()
+        monkeypatch.setenv("IRLMX_TEST_DROP_TILE", "1")
+        monkeypatch.setenv("IRLMX_TEST_EXCHANGE_TIMEOUT_MS", "50")
+        got = run()
+        after = ops.counters()
+        assert after["rerun_timeout"] == before["rerun_timeout"] + 1, op
+        assert after["sweep_calls"] == before["sweep_calls"] + 1, op
+        for x, y in zip(got if isinstance(got, tuple) else (got,), ref if isinstance(ref, tuple) else (ref,)):
+            assert torch.equal(x, y), op
+        monkeypatch.setenv("IRLMX_STRICT_EXCHANGE", "1")
+        with pytest.raises(_lib.IrlmxError, match="dense grid shape: exchange timed out"):
+            run()
+        for k in ("IRLMX_TEST_DROP_TILE", "IRLMX_TEST_EXCHANGE_TIMEOUT_MS", "IRLMX_STRICT_EXCHANGE"):
+            monkeypatch.delenv(k)
+    torch.cuda.synchronize()
 
 
 BELLMAN_CASES = [  # S, A, B, shared

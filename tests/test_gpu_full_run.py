@@ -39,7 +39,7 @@ def staggered_workload(dev, size, n_inst, seed0=100, offset=1e-3):
     e_f = np.empty((n_inst, S))
     p0 = np.empty((n_inst, S))
     for b in range(n_inst):
-        e_f[b], p0[b], _ = demos.sample(rv[b], size, [S - 1], 0, n=50, seed=seed0 + b)
+        e_f[b], p0[b], _ = demos.sample(rv[b], size, [S - 1], 0, n=50, seed=seed0 + b, max_len=demos.safety_cap(size))
     svf0 = BatchedMaxEnt(mdp, e_f, p0, [S - 1]).step().cpu().numpy()   # SVF at theta0 = 1
     e_f[0] = svf0[0]
     e_f[1] = svf0[1] + offset
@@ -112,7 +112,7 @@ def test_run_matches_oracle_irl_loop(dev):
     e_f = np.empty((3, S))
     p0 = np.empty((3, S))
     for b in range(3):
-        e_f[b], p0[b], _ = demos.sample(rv[b], size, [S - 1], 0, n=40, seed=9 + b)
+        e_f[b], p0[b], _ = demos.sample(rv[b], size, [S - 1], 0, n=40, seed=9 + b, max_len=demos.safety_cap(size))
     irl = BatchedMaxEnt(mdp, e_f, p0, [S - 1])
     r, k = irl.run(eps=1e-4)
     for b in range(3):
@@ -137,3 +137,69 @@ def test_run_matches_oracle_irl_loop(dev):
     for b in (0, 2):
         assert int(k[b]) == int(z["irl_steps"])
         assert np.max(np.abs(r[b].cpu().numpy() - z["reward_maxent"])) <= 1e-9
+
+
+def test_batched_optimizers_match_reference(dev):
+    """BatchedMaxEnt with the reference's other optimisers on the device
+    (irlmx.optim: Sga, NormalizeGrad with ord None / 1, ExpSga with normalize,
+    power / exponential decay, a Uniform-drawn theta0; optimizer.py:61-398)
+    against the reference's own full irl / irl_causal runs
+    (tests/golden/optimizers.npz): step counts identical, rewards within 1e-9;
+    two instances per batch, both equal to the single reference run."""
+    from irlmx import DeviceMDP
+    from irlmx import optim as OP
+    from irlmx.batch import BatchedMaxEnt
+    z = load_golden("optimizers")
+    c1 = load_golden("config1")
+    make = {
+        "sga_power": lambda: OP.Sga(lr=OP.power_decay(lr0=0.2, power=2)),
+        "sga_linear": lambda: OP.Sga(lr=OP.linear_decay(lr0=0.2)),
+        "expsga_expdecay": lambda: OP.ExpSga(lr=OP.exponential_decay(lr0=0.2, decay_rate=0.01)),
+        "norm_expsga": lambda: OP.NormalizeGrad(OP.ExpSga(lr=OP.linear_decay(lr0=0.2))),
+        "norm1_sga": lambda: OP.NormalizeGrad(OP.Sga(lr=OP.power_decay(lr0=0.5, decay_steps=2, power=1.5)), ord=1),
+        "expsga_normalize_uniform": lambda: OP.ExpSga(lr=OP.linear_decay(lr0=0.2), normalize=True),
+        "causal_norm1_sga": lambda: OP.NormalizeGrad(OP.Sga(lr=OP.power_decay(lr0=0.5, decay_steps=2, power=1.5)),
+                                                     ord=1),
+    }
+    assert sorted(make) == sorted(str(n) for n in z["names"])
+    mdp = DeviceMDP.icy_gridworld(5, [0.2, 0.2], device=dev)
+    e_f = np.tile(c1["e_features"], (2, 1))
+    p0 = np.tile(c1["p_initial"], (2, 1))
+    for name, mk in make.items():
+        causal = name.startswith("causal")
+        irl = BatchedMaxEnt(mdp, e_f, p0, [24], causal=causal, discount=0.7 if causal else None,
+                            theta0=z[name + "__theta0"], optimizer=mk())
+        r, k = irl.run(eps=1e-4, max_steps=5000)
+        assert k.tolist() == [int(z[name + "__steps"])] * 2, (name, k.tolist())
+        for b in range(2):
+            err = np.max(np.abs(r[b].cpu().numpy() - z[name + "__reward"]))
+            assert err <= 1e-9 * max(1.0, np.max(np.abs(z[name + "__reward"]))), (name, b, err)
+
+
+def test_dense_compaction_within_rounding(dev):
+    """DENSE layout (irlmx/batch.py docstring): a compacted run re-plans from
+    the shared-table GEMM (20 instances) down to the streaming / dense-grid
+    kernels as instances stop, whose per-row summation orders differ -- the
+    run agrees with the uncompacted one to 1e-9 (steps per instance equal),
+    not bit for bit."""
+    from irlmx import DeviceMDP, demos, ops
+    from irlmx.batch import BatchedMaxEnt
+    size, S, B = 6, 36, 20
+    P = O.icy_gridworld_table(size, 0.2)
+    grid = DeviceMDP.icy_gridworld(size, 0.2, device=dev)
+    rv = grid.row_val.cpu().numpy()
+    e_f = np.empty((B, S))
+    p0 = np.empty((B, S))
+    for b in range(B):
+        e_f[b], p0[b], _ = demos.sample(rv[0], size, [S - 1], 0, n=30, seed=100 + b, max_len=demos.safety_cap(size))
+    mdp = DeviceMDP.from_dense(P, device=dev, layout="dense").with_batch(B)
+    assert ops.execution_plan(mdp, "backward")["shape"] == "dense-gemm"
+    runs = {}
+    for compact in (True, False):
+        irl = BatchedMaxEnt(mdp, e_f, p0, [S - 1])
+        runs[compact] = irl.run(eps=1e-4, compact=compact)
+    (r1, k1), (r0, k0) = runs[True], runs[False]
+    assert len(set(k0.tolist())) > 1                 # instances stop at different steps
+    assert torch.equal(k1, k0), (k1.tolist(), k0.tolist())
+    err = (r1 - r0).abs().max().item() / r0.abs().max().item()
+    assert err <= 1e-9, err

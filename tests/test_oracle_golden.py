@@ -264,3 +264,43 @@ def test_demos_truncation_reported():
     e_f, _, lens5, cut = demos.sample(rv, size, [n - 1], 0, n=20, seed=3, max_len=5, on_truncate="allow",
                                       with_truncated=True)
     assert cut == 20 and int(lens5.max()) == 5 and abs(e_f.sum() - 6.0) < 1e-12   # 5 steps + the cut state
+
+
+def _optimizer_cases():
+    z = load_golden("optimizers")
+    make = {
+        "sga_power": (lambda: O.Sga(lr=O.power_decay(lr0=0.2, power=2)), lambda: O.Constant(1.0)),
+        "sga_linear": (lambda: O.Sga(lr=O.linear_decay(lr0=0.2)), lambda: O.Constant(1.0)),
+        "expsga_expdecay": (lambda: O.ExpSga(lr=O.exponential_decay(lr0=0.2, decay_rate=0.01)),
+                            lambda: O.Constant(1.0)),
+        "norm_expsga": (lambda: O.NormalizeGrad(O.ExpSga(lr=O.linear_decay(lr0=0.2))), lambda: O.Constant(1.0)),
+        "norm1_sga": (lambda: O.NormalizeGrad(O.Sga(lr=O.power_decay(lr0=0.5, decay_steps=2, power=1.5)), ord=1),
+                      lambda: O.Constant(1.0)),
+        "expsga_normalize_uniform": (lambda: O.ExpSga(lr=O.linear_decay(lr0=0.2), normalize=True),
+                                     lambda: O.Uniform(0.5, 1.5)),
+        "causal_norm1_sga": (lambda: O.NormalizeGrad(O.Sga(lr=O.power_decay(lr0=0.5, decay_steps=2, power=1.5)),
+                                                     ord=1), lambda: O.Constant(1.0)),
+    }
+    assert sorted(make) == sorted(str(n) for n in z["names"])
+    return z, make
+
+
+@pytest.mark.slow
+def test_oracle_optimizers_match_reference():
+    """The oracle's Sga, NormalizeGrad, ExpSga(normalize), power / exponential
+    decay and Uniform (optimizer.py:61-398) reproduce the reference's full irl /
+    irl_causal runs of tests/golden/optimizers.npz (tools/gen_golden.py) bit for bit."""
+    z, make = _optimizer_cases()
+    c1 = load_golden("config1")
+    tjs = unpack_trajectories(c1["traj_flat"], c1["traj_lens"])
+    P, feats = c1["p_transition"], np.identity(25)
+    for name in ("sga_power", "norm1_sga", "expsga_normalize_uniform", "causal_norm1_sga"):
+        mk_opt, mk_init = make[name]
+        np.random.seed(7)
+        assert np.array_equal(mk_init()(25), z[name + "__theta0"]), name
+        np.random.seed(7)
+        if name.startswith("causal"):
+            r, k = O.irl_causal(P, feats, [24], tjs, mk_opt(), mk_init(), 0.7)
+        else:
+            r, k = O.irl(P, feats, [24], tjs, mk_opt(), mk_init())
+        assert k == int(z[name + "__steps"]) and np.array_equal(r, z[name + "__reward"]), name

@@ -15,7 +15,7 @@ mdp = DeviceMDP.icy_gridworld(size, instance_slips(np.arange(B), B), device=dev)
 rv = mdp.row_val.cpu().numpy()
 e_f = np.empty((B, S)); p0 = np.empty((B, S))
 for b in range(B):
-    e_f[b], p0[b], _ = demos.sample(rv[b], size, [S - 1], 0, n=200, seed=1234 + b)
+    e_f[b], p0[b], _ = demos.sample(rv[b], size, [S - 1], 0, n=200, seed=1234 + b, max_len=demos.safety_cap(size))
 print("setup", time.time() - t, flush=True)
 if hasattr(irlmx._lib.load(), "irlmx_execution_plan"):
     print("plans", ops.execution_plan(mdp, "backward"), ops.execution_plan(mdp, "forward"), flush=True)

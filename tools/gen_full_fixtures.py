@@ -71,7 +71,7 @@ def bench_instance(size, b, n_total):
     mats = O.icy_gridworld_csr(size, slip)
     rv = O.stencil_row_val(mats, size)
     n = size * size
-    e_f, p0, _ = demos.sample(rv, size, [n - 1], 0, n=200, seed=1234 + b)
+    e_f, p0, _ = demos.sample(rv, size, [n - 1], 0, n=200, seed=1234 + b, max_len=demos.safety_cap(size))
     return slip, mats, e_f, p0
 
 

@@ -335,8 +335,68 @@ def gen_causal_128():
     save("causal_128", theta=theta, pi=pi, k_s=k_s, size=size, discount=0.7)
 
 
+class Counting:
+    """Wraps a reference optimizer and counts its steps (outer IRL iterations)."""
+
+    def __init__(self, opt):
+        self.opt, self.n_steps = opt, 0
+
+    def reset(self, parameters):
+        self.opt.reset(parameters)
+
+    def step(self, grad, *args, **kwargs):
+        self.n_steps += 1
+        return self.opt.step(grad, *args, **kwargs)
+
+
+# the reference's other optimizers, schedules and initialisers (optimizer.py:61-108,
+# 110-167, 170-214, 217-293, 334-398) on config 1's world and demonstrations
+OPT_CASES = {
+    "sga_power": (lambda: O.Sga(lr=O.power_decay(lr0=0.2, power=2)), lambda: O.Constant(1.0), False),
+    "sga_linear": (lambda: O.Sga(lr=O.linear_decay(lr0=0.2)), lambda: O.Constant(1.0), False),
+    "expsga_expdecay": (lambda: O.ExpSga(lr=O.exponential_decay(lr0=0.2, decay_rate=0.01)),
+                        lambda: O.Constant(1.0), False),
+    "norm_expsga": (lambda: O.ExpSga(lr=O.linear_decay(lr0=0.2)).normalize_grad(), lambda: O.Constant(1.0), False),
+    "norm1_sga": (lambda: O.NormalizeGrad(O.Sga(lr=O.power_decay(lr0=0.5, decay_steps=2, power=1.5)), ord=1),
+                  lambda: O.Constant(1.0), False),
+    "expsga_normalize_uniform": (lambda: O.ExpSga(lr=O.linear_decay(lr0=0.2), normalize=True),
+                                 lambda: O.Uniform(0.5, 1.5), False),
+    "causal_norm1_sga": (lambda: O.NormalizeGrad(O.Sga(lr=O.power_decay(lr0=0.5, decay_steps=2, power=1.5)),
+                                                 ord=1), lambda: O.Constant(1.0), True),
+}
+
+
+def gen_optimizers():
+    """G7: full irl / irl_causal runs with the reference's other optimizers
+    (Sga, NormalizeGrad, ExpSga(normalize), power / exponential decay, Uniform
+    init seeded with np.random.seed(7)) on config 1's world and demonstrations."""
+    world = W.IcyGridWorld(size=5, p_slip=0.2)
+    z = np.load(os.path.join(OUT, "config1.npz"))
+    flat, lens = z["traj_flat"], z["traj_lens"]
+    tjs, o = [], 0
+    for n in lens:
+        tjs.append(T.Trajectory([tuple(int(v) for v in row) for row in flat[o:o + n]]))
+        o += n
+    features = W.state_features(world)
+    out = {"names": np.array(list(OPT_CASES))}
+    for name, (make_opt, make_init, causal) in OPT_CASES.items():
+        np.random.seed(7)
+        theta0 = make_init()(world.n_states)
+        np.random.seed(7)
+        opt = Counting(make_opt())
+        if causal:
+            r = M.irl_causal(world.p_transition, features, [24], tjs, opt, make_init(), 0.7)
+        else:
+            r = M.irl(world.p_transition, features, [24], tjs, opt, make_init())
+        out[name + "__theta0"] = theta0
+        out[name + "__reward"] = r
+        out[name + "__steps"] = opt.n_steps
+        print(f"optimizers: {name} {opt.n_steps} steps")
+    save("optimizers", **out)
+
+
 GENS = {"config1": gen_config1, "maxent_small": gen_maxent_small, "causal_small": gen_causal_small,
-        "worlds": gen_worlds, "vi": gen_vi, "generic": gen_generic}
+        "worlds": gen_worlds, "vi": gen_vi, "generic": gen_generic, "optimizers": gen_optimizers}
 HEAVY = {"causal_128": gen_causal_128}
 
 
