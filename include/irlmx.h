@@ -171,6 +171,19 @@ int irlmx_forward_svf(const irlmx_mdp* mdp, const double* p_initial, const uint8
                       size_t workspace_bytes, void* stream);
 
 /*
+ * The same forward pass in numpy's own floating-point order (no reference
+ * counterpart beyond maxent.py:105-114 itself): x_a = pi[:, a] * d, every
+ * P'_a^T . x_a summed as numpy's OpenBLAS dgemv_n sums it on a Haswell-family
+ * x86-64 host (groups of four sources, see oracle/blas_order.c), the sequential
+ * action sum, + p_initial, delta = max|d_ - d| -- so the SVF and the sweep
+ * count are bit-identical to the reference's there.  One workgroup per
+ * instance.  Requires S <= 4096, S % 4 in {0, 1} and (ELL) k_col <= 32.
+ */
+int irlmx_forward_svf_numpy_order(const irlmx_mdp* mdp, const double* p_initial, const uint8_t* terminal,
+                                  const double* p_action, double eps, int64_t max_iter, double* svf,
+                                  int64_t* iterations, int32_t* status, void* stream);
+
+/*
  * MaxCausalEnt soft value iteration -- replaces
  * maxent.local_causal_action_probabilities (reference src/maxent.py:279-341).
  *   reward [B][S]; terminal_reward [B][S] = phi (-inf except 0 at terminals, or

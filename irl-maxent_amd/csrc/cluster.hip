@@ -949,11 +949,17 @@ bool cluster_plan(int W, int H, int B, int mode, ClusterPlan* out) {
       // 64x64 instance, C = 8..32: tools/diag/plan_bench.py)
       if (mode == kModeFwd && !solo) xchg += 120.0 * (C - 16);
       // (the forward's convergence bookkeeping: ~165 cycles per slot)
-      const double cost = nl * (std::max((mode == kModeFwd ? 165.0 : 110.0) * spt, 850.0) * G + xchg) / G;
+      // A solo tile has no ghost rows, so its block length is free: the backward
+      // runs blocks of kSoloBwdT sweeps (IRLMX_SOLO_T; the growth cap still
+      // bounds it), amortising the ~1.9k cycles of per-block bookkeeping
+      // (rescale test, summary, register refresh) over 4x more sweeps.  (The
+      // forward's per-sweep convergence bits hold 16 sweeps per block.)
+      const int T = (solo && mode == kModeBwd) ? std::max(1, env_int("IRLMX_SOLO_T", kSoloBwdT)) : G;
+      const double cost = nl * (std::max((mode == kModeFwd ? 165.0 : 110.0) * spt, 850.0) * T + xchg) / T;
       if (cost < best - 1e-9) {
         best = cost;
         ok = true;
-        *out = ClusterPlan{R, G, C, G, std::min(per, B), spt, spt * nt, lds, layout, nt};
+        *out = ClusterPlan{R, G, C, T, std::min(per, B), spt, spt * nt, lds, layout, nt};
       }
     }
   }

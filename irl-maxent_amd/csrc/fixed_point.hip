@@ -537,6 +537,169 @@ __device__ double np_row_dot(const Model& m, int b, int a, int s, const double* 
   return y;
 }
 
+// p'[a][:, t] . x in OpenBLAS dgemv_n order (numpy's P_a.T.dot(x), maxent.py:109;
+// oracle/blas_order.c blas_order_dgemv_cols): for t < S & ~3 the sources in
+// groups of four, each group one chain c = fma(.., c) in source order 4g + 1,
+// 4g, 4g + 2, 4g + 3 (its first term a rounded product), added to the sum group
+// after group; a last source s = S - 1 (S % 4 == 1) as a rounded product added
+// last; the last output t = S - 1 one fma chain over the sources in order.
+// Zero entries (terminal sources, unused slots) are exact no-ops while x is
+// finite, so only stored entries are visited.  xs(s) = pi[s, a] * d[s], rounded.
+constexpr int kNpColMax = 32;  // ELL column slots the numpy-order forward supports
+
+template <int LAYOUT, typename XS>
+__device__ double np_col_dot(const Model& m, int b, int a, int t, const uint8_t* term, XS xs) {
+  const int S = m.S, n4 = S & ~3;
+  if (LAYOUT == IRLMX_LAYOUT_DENSE) {
+    const double* col = m.row_val + (inst_of(m, b) * m.A + a) * (size_t)S * S + t;  // P[s, t, a] at s * S
+    auto v = [&](int s) { return term[s] ? 0.0 : col[(size_t)s * S]; };
+    double out = 0.0;
+    if (t >= n4) {
+      for (int s = 0; s < S; ++s) out = fma(v(s), xs(s), out);
+      return out;
+    }
+    for (int s = 0; s < n4; s += 4) {
+      double c = __dmul_rn(v(s + 1), xs(s + 1));
+      c = fma(v(s), xs(s), c);
+      c = fma(v(s + 2), xs(s + 2), c);
+      c = fma(v(s + 3), xs(s + 3), c);
+      out = __dadd_rn(out, c);
+    }
+    for (int s = n4; s < S; ++s) out = __dadd_rn(out, __dmul_rn(v(s), xs(s)));
+    return out;
+  }
+  // stored entries of column t, ascending by source
+  constexpr int KM = LAYOUT == IRLMX_LAYOUT_STENCIL5 ? kStencilK : kNpColMax;
+  int src[KM];
+  double val[KM];
+  int n = 0;
+  if (LAYOUT == IRLMX_LAYOUT_STENCIL5) {
+    constexpr int order[kStencilK] = {4, 2, 0, 1, 3};  // sources t - W, t - 1, t, t + 1, t + W
+#pragma unroll
+    for (int i = 0; i < kStencilK; ++i) {
+      const int k = order[i];
+      if (!stencil_valid(t, k, m.W, m.H)) continue;
+      const int s = stencil_nbr(t, k, m.W, m.H);
+      if (term[s]) continue;
+      src[n] = s;
+      val[n] = row_val(m, b, a, stencil_opposite(k), s);  // P[s, t, a]
+      ++n;
+    }
+  } else {
+    for (int k = 0; k < m.Kc && k < kNpColMax; ++k) {
+      const int s = col_src(m, b, t, k);
+      const double v = m.col_val[((inst_of(m, b) * m.A + a) * m.Kc + k) * S + t];
+      if (term[s] || v == 0.0) continue;
+      int j = n++;  // insertion by source (unused slots repeat t with value 0 and are skipped)
+      for (; j > 0 && src[j - 1] > s; --j) { src[j] = src[j - 1]; val[j] = val[j - 1]; }
+      src[j] = s;
+      val[j] = v;
+    }
+  }
+  double out = 0.0;
+  if (t >= n4) {
+    for (int i = 0; i < n; ++i) out = fma(val[i], xs(src[i]), out);
+    return out;
+  }
+  int i = 0;
+  while (i < n && src[i] < n4) {
+    const int g = src[i] >> 2;
+    int e = i;
+    while (e < n && src[e] < n4 && (src[e] >> 2) == g) ++e;
+    double c = 0.0;
+    constexpr int qorder[4] = {1, 0, 2, 3};
+#pragma unroll
+    for (int qi = 0; qi < 4; ++qi)
+      for (int j = i; j < e; ++j)
+        if ((src[j] & 3) == qorder[qi]) c = fma(val[j], xs(src[j]), c);
+    out = __dadd_rn(out, c);
+    i = e;
+  }
+  for (; i < n; ++i) out = __dadd_rn(out, __dmul_rn(val[i], xs(src[i])));
+  return out;
+}
+
+struct NpFwdArgs {
+  Model m;
+  const double* p0;     // [B][S]
+  const uint8_t* term;  // [B][S]
+  const double* pi;     // [B][S][A]
+  double eps;
+  long long max_iter;
+  double* svf;          // [B][S]
+  int64_t* iters;
+  int32_t* status;
+};
+
+// Forward in numpy's order (irlmx_forward_svf_numpy_order): maxent.py:105-114
+// with every rounding where numpy puts it -- x_a = pi[:, a] * d, y_a = P'_a^T x_a
+// (np_col_dot), d_ = p0 + (((y_0 + y_1) + y_2) + ...), delta = max|d_ - d| -- so
+// the SVF and the sweep count are bit-identical to the reference's on a
+// Haswell-family host.  A non-finite policy or value meets the zero entries of
+// the dense product (0 * NaN): every later entry is NaN, as in the reference.
+template <int LAYOUT>
+__global__ void __launch_bounds__(1024) fwd_numpy_order_kernel(NpFwdArgs a) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  const Model& m = a.m;
+  const int S = m.S, A = m.A;
+  const int b = blockIdx.x, tid = threadIdx.x, nt = blockDim.x;
+  double* buf[2] = {(double*)smem, (double*)smem + S};
+  unsigned long long* slot = (unsigned long long*)(buf[1] + S);  // [3] delta ring
+  int* bad = (int*)(slot + 3);                                     // [2] sticky non-finite, by parity
+  const double* pi = a.pi + (size_t)b * S * A;
+  const double* p0 = a.p0 + (size_t)b * S;
+  const uint8_t* term = a.term + (size_t)b * S;
+  bool nf = false;
+  for (int s = tid; s < S; s += nt) {
+    buf[0][s] = 0.0;  // maxent.py:105
+    for (int act = 0; act < A; ++act) nf |= !isfinite(pi[(size_t)s * A + act]);
+  }
+  if (tid < 3) slot[tid] = 0ull;
+  if (tid < 2) bad[tid] = 0;
+  __syncthreads();
+  if (nf) bad[1] = 1;  // a non-finite policy: the first sweep's product is NaN everywhere
+  __syncthreads();
+  long long it = 0;
+  int r3 = 0;
+  double delta = 0.0;
+  for (;;) {
+    const double* d = buf[it & 1];
+    double* dn = buf[(it & 1) ^ 1];
+    const bool poisoned = bad[(it & 1) ^ 1] != 0;  // written in the previous sweep (or above)
+    unsigned long long mx = 0ull;
+    bool nfo = false;
+    for (int t = tid; t < S; t += nt) {
+      double v = 0.0;
+      for (int act = 0; act < A; ++act) {
+        auto xs = [&](int s) { return __dmul_rn(pi[(size_t)s * A + act], d[s]); };  // maxent.py:109
+        const double y = poisoned ? kNaN : np_col_dot<LAYOUT>(m, b, act, t, term, xs);
+        v = act == 0 ? y : __dadd_rn(v, y);  // np.array(d_).sum(axis=0)
+      }
+      const double nv = __dadd_rn(p0[t], v);  // maxent.py:110
+      dn[t] = nv;
+      nfo |= !isfinite(nv);
+      const unsigned long long dd = abs_bits(nv - d[t]);
+      mx = dd > mx ? dd : mx;
+    }
+    if (nfo) bad[it & 1] = 1;
+    mx = wave_max_u64(mx);
+    if ((tid & (kWave - 1)) == 0 && mx) atomicMax(&slot[r3], mx);
+    if (tid == 0) slot[r3 == 2 ? 0 : r3 + 1] = 0ull;
+    __syncthreads();
+    delta = bits_double(slot[r3]);
+    r3 = r3 == 2 ? 0 : r3 + 1;
+    ++it;
+    if (!(delta > a.eps)) break;  // maxent.py:108
+    if (a.max_iter > 0 && it >= a.max_iter) break;
+  }
+  const double* d = buf[it & 1];
+  for (int t = tid; t < S; t += nt) a.svf[(size_t)b * S + t] = d[t];
+  if (tid == 0) {
+    a.iters[b] = it;
+    a.status[b] = finish_status(delta, a.eps);
+  }
+}
+
 template <int LAYOUT>
 __global__ void __launch_bounds__(1024) bwd_numpy_order_kernel(NpArgs a) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
@@ -2184,6 +2347,38 @@ extern "C" int irlmx_value_iteration(const irlmx_mdp* mdp, const double* reward,
                                      int32_t* status, void* workspace, size_t workspace_bytes, void* stream) {
   return bellman_common(mdp, reward, nullptr, discount, eps, max_iter, average, nullptr, value, iterations,
                         status, workspace, workspace_bytes, stream, false);
+}
+
+extern "C" int irlmx_forward_svf_numpy_order(const irlmx_mdp* mdp, const double* p_initial,
+                                             const uint8_t* terminal, const double* p_action, double eps,
+                                             int64_t max_iter, double* svf, int64_t* iterations, int32_t* status,
+                                             void* stream) {
+  if (int rc = validate(mdp)) return rc;
+  const Model m = make_model(mdp);
+  if (int rc = need_all("forward_svf_numpy_order", {{p_initial, "p_initial"}, {terminal, "terminal"},
+                                                    {p_action, "p_action"}, {svf, "svf"},
+                                                    {iterations, "iterations"}, {status, "status"}}))
+    return rc;
+  if (m.S > kFusedMaxStates || (m.S & 3) > 1) {
+    set_error("forward_svf_numpy_order: numpy's order is restated for S <= %d with S %% 4 in {0, 1}, got S=%d",
+              kFusedMaxStates, m.S);
+    return IRLMX_EINVAL;
+  }
+  if (mdp->layout == IRLMX_LAYOUT_ELL && (!m.col_idx || !m.col_val || m.Kc <= 0 || m.Kc > kNpColMax)) {
+    set_error("forward_svf_numpy_order: ELL column form missing or k_col > %d", kNpColMax);
+    return IRLMX_EINVAL;
+  }
+  NpFwdArgs a{m, p_initial, terminal, p_action, eps, (long long)max_iter, svf, iterations, status};
+  void (*k)(NpFwdArgs) = m.stencil ? fwd_numpy_order_kernel<IRLMX_LAYOUT_STENCIL5>
+                                   : (m.dense ? fwd_numpy_order_kernel<IRLMX_LAYOUT_DENSE>
+                                              : fwd_numpy_order_kernel<IRLMX_LAYOUT_ELL>);
+  const size_t lds = 2 * (size_t)m.S * sizeof(double) + 3 * sizeof(unsigned long long) + 2 * sizeof(int);
+  hipError_t e = hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+  if (e != hipSuccess) return hip_fail(e, "hipFuncSetAttribute");
+  hipLaunchKernelGGL(k, dim3(m.B), dim3(m.S >= 1024 ? 1024 : ((m.S + kWave - 1) / kWave) * kWave), lds,
+                     (hipStream_t)stream, a);
+  e = hipGetLastError();
+  return e == hipSuccess ? 0 : hip_fail(e, "forward_svf_numpy_order");
 }
 
 // Soft VI / VI in numpy's order: one workgroup per instance (S <= 4096, S % 4 in {0, 1}).

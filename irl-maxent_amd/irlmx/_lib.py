@@ -72,6 +72,7 @@ SIGNATURES = {
     "irlmx_device_check_failures": (_I64, []),
     "irlmx_backward_maxent": (ctypes.c_int, [_MDP, _P, _P, _I32, _P, _P, _P, _SZ, _P]),
     "irlmx_backward_maxent_numpy_order": (ctypes.c_int, [_MDP, _P, _P, _P, _P, _P]),
+    "irlmx_forward_svf_numpy_order": (ctypes.c_int, [_MDP, _P, _P, _P, _D, _I64, _P, _P, _P, _P]),
     "irlmx_forward_svf": (ctypes.c_int, [_MDP, _P, _P, _P, _D, _I64, _P, _P, _P, _P, _SZ, _P]),
     "irlmx_soft_backward": (ctypes.c_int, [_MDP, _P, _P, _D, _D, _I64, _P, _P, _P, _P, _P, _SZ, _P]),
     "irlmx_soft_backward_numpy_order": (ctypes.c_int, [_MDP, _P, _P, _D, _D, _I64, _P, _P, _P, _P, _P]),

@@ -100,10 +100,14 @@ def backward_maxent(mdp, reward, terminal, rescale=True):
     return pi
 
 
-def numpy_order_supported(mdp):
-    """Whether backward_maxent_numpy_order covers this model (S <= 4096, S % 4 in {0, 1})."""
+def numpy_order_supported(mdp, op="backward"):
+    """Whether the numpy-order kernels cover this model (S <= 4096, S % 4 in
+    {0, 1}; the forward's ELL column form at most 32 slots)."""
     S = mdp.n_states
-    return S <= 4096 and S % 4 in (0, 1)
+    ok = S <= 4096 and S % 4 in (0, 1)
+    if op == "forward" and mdp.layout == _lib.LAYOUT_ELL:
+        ok = ok and mdp.k_col <= 32
+    return ok
 
 
 def backward_maxent_numpy_order(mdp, exp_reward, terminal):
@@ -123,10 +127,12 @@ def backward_maxent_numpy_order(mdp, exp_reward, terminal):
     return pi
 
 
-def forward_svf(mdp, p_initial, terminal, p_action, eps=1e-5, max_iter=0):
+def forward_svf(mdp, p_initial, terminal, p_action, eps=1e-5, max_iter=0, numpy_order=False):
     """Expected state-visitation frequencies (maxent.py:63-114).
 
     Returns ``(svf [B, S], iterations [B] int64, status [B] int32)``.
+    ``numpy_order``: numpy's summation order (irlmx_forward_svf_numpy_order):
+    SVF and sweep count bit-identical to the reference on a Haswell-family host.
     """
     lib = _lib.load()
     B, S, A = mdp.batch, mdp.n_states, mdp.n_actions
@@ -136,6 +142,12 @@ def forward_svf(mdp, p_initial, terminal, p_action, eps=1e-5, max_iter=0):
     svf = torch.empty((B, S), dtype=torch.float64, device=mdp.device)
     iters = torch.empty(B, dtype=torch.int64, device=mdp.device)
     status = torch.empty(B, dtype=torch.int32, device=mdp.device)
+    if numpy_order:
+        _lib.check(lib.irlmx_forward_svf_numpy_order(mdp.struct(), _lib.ptr(p0), _lib.ptr(term), _lib.ptr(pi),
+                                                     float(eps), int(max_iter), _lib.ptr(svf), _lib.ptr(iters),
+                                                     _lib.ptr(status), _lib.stream_ptr(mdp.device)),
+                   "forward_svf_numpy_order")
+        return svf, iters, status
     ws, n = _workspace(mdp, _lib.OP_FORWARD)
     _lib.check(lib.irlmx_forward_svf(mdp.struct(), _lib.ptr(p0), _lib.ptr(term), _lib.ptr(pi), float(eps),
                                      int(max_iter), _lib.ptr(svf), _lib.ptr(iters), _lib.ptr(status),

@@ -99,15 +99,23 @@ def expected_svf_from_policy(p_transition, p_initial, terminal, p_action, eps=1e
     """Expected state visitation frequencies under ``p_action`` (maxent.py:63-114)."""
     mdp = _model(p_transition)
     term = ops.terminal_mask(terminal, mdp.n_states, device=mdp.device)
-    svf, _, _ = ops.forward_svf(mdp, p_initial, term, p_action, eps)
+    svf, _, _ = _forward(mdp, p_initial, term, p_action, eps)
     return _host(svf)
 
 
-def _np_order(mdp):
+def _np_order(mdp, op="backward"):
     """numpy's own summation order for this call (one instance, a model the
-    numpy-order kernels cover; IRLMX_NUMPY_ORDER=0 turns it off)."""
-    return (mdp.batch == 1 and ops.numpy_order_supported(mdp)
-            and os.environ.get("IRLMX_NUMPY_ORDER", "1") != "0")
+    numpy-order kernels cover; IRLMX_NUMPY_ORDER=0 turns it off).  The forward
+    runs in numpy's order up to 1024 states (IRLMX_NUMPY_ORDER_FWD_MAX): its
+    one-workgroup kernel is slower per sweep than the tiled shapes, and larger
+    worlds run 10^5-10^6 sweeps (where the reference itself takes hours)."""
+    if mdp.batch != 1 or not ops.numpy_order_supported(mdp, op) or os.environ.get("IRLMX_NUMPY_ORDER", "1") == "0":
+        return False
+    return op != "forward" or mdp.n_states <= int(os.environ.get("IRLMX_NUMPY_ORDER_FWD_MAX", "1024"))
+
+
+def _forward(mdp, p_initial, term, pi, eps):
+    return ops.forward_svf(mdp, p_initial, term, pi, eps, numpy_order=_np_order(mdp, "forward"))
 
 
 def _backward(mdp, reward, term):
@@ -133,7 +141,7 @@ def compute_expected_svf(p_transition, p_initial, terminal, reward, eps=1e-5):
     mdp = _model(p_transition)
     term = ops.terminal_mask(terminal, mdp.n_states, device=mdp.device)
     pi = _backward(mdp, reward, term)
-    svf, _, _ = ops.forward_svf(mdp, p_initial, term, pi, eps)
+    svf, _, _ = _forward(mdp, p_initial, term, pi, eps)
     return _host(svf)
 
 
@@ -173,7 +181,7 @@ def irl(p_transition, features, terminal, trajectories, optim, init, eps=1e-4, e
 
     def svf_fn(m, reward, term, p0):
         pi = _backward(m, reward, term)
-        svf, _, _ = ops.forward_svf(m, p0, term, pi, eps_esvf)
+        svf, _, _ = _forward(m, p0, term, pi, eps_esvf)
         return _host(svf)
 
     return _irl_loop(mdp, features, terminal, trajectories, optim, init, eps, svf_fn)
@@ -212,7 +220,7 @@ def compute_expected_causal_svf(p_transition, p_initial, terminal, reward, disco
     phi = _terminal_reward(terminal, mdp.n_states)
     pi, _, _, _ = ops.soft_backward(mdp, reward, phi, discount, eps_lap, numpy_order=_np_order(mdp))
     term = ops.terminal_mask(terminal, mdp.n_states, device=mdp.device)
-    svf, _, _ = ops.forward_svf(mdp, p_initial, term, pi, eps_svf)
+    svf, _, _ = _forward(mdp, p_initial, term, pi, eps_svf)
     return _host(svf)
 
 
@@ -224,7 +232,7 @@ def irl_causal(p_transition, features, terminal, trajectories, optim, init, disc
 
     def svf_fn(m, reward, term, p0):
         pi, _, _, _ = ops.soft_backward(m, reward, phi, discount, eps_lap, numpy_order=_np_order(m))
-        svf, _, _ = ops.forward_svf(m, p0, term, pi, eps_svf)
+        svf, _, _ = _forward(m, p0, term, pi, eps_svf)
         return _host(svf)
 
     return _irl_loop(mdp, features, terminal, trajectories, optim, init, eps, svf_fn)

@@ -143,3 +143,78 @@ long long blas_order_value_iteration(const double* P, int S, int A, const double
   free(pa); free(q); free(vo);
   return it;
 }
+
+/*
+ * y[t] = sum_s M[s][t] x[s] -- numpy's M.T.dot(x) for a C-contiguous square M
+ * (maxent.py:109: p_transition[a].T.dot(...)), i.e. OpenBLAS dgemv_n on the
+ * column-major view, in its Haswell order (probed like dgemv_t above): for
+ * outputs t < n & ~3, per group of four sources s = 4g .. 4g + 3 a chain
+ * round(a1 x1), fma a0, fma a2, fma a3, added to y group after group, then the
+ * remaining n % 4 sources as rounded products added one by one; the last
+ * n % 4 outputs one fma chain over all sources in order.
+ */
+int blas_order_dgemv_cols(const double* M, int n, const double* x, double* y) {
+  if (n <= 0 || (n & 3) > 1) return -1;
+  const int n4 = n & ~3;
+  for (int t = 0; t < n; ++t) {
+    double out = 0.0;
+    if (t >= n4) {
+      for (int s = 0; s < n; ++s) out = fma(M[(size_t)s * n + t], x[s], out);
+    } else {
+      for (int s = 0; s < n4; s += 4) {
+        double c = M[(size_t)(s + 1) * n + t] * x[s + 1];
+        c = fma(M[(size_t)s * n + t], x[s], c);
+        c = fma(M[(size_t)(s + 2) * n + t], x[s + 2], c);
+        c = fma(M[(size_t)(s + 3) * n + t], x[s + 3], c);
+        out = out + c;
+      }
+      for (int s = n4; s < n; ++s) out = out + M[(size_t)s * n + t] * x[s];
+    }
+    y[t] = out;
+  }
+  return 0;
+}
+
+/*
+ * expected_svf_from_policy (maxent.py:63-114) in that order: P' = P with the
+ * terminal rows zeroed (98-99); per sweep x_a = pi[:, a] * d (rounded),
+ * y_a = P'_a^T . x_a (blas_order_dgemv_cols), d_ = p0 + (((y_0 + y_1) + y_2) + ...)
+ * (np.array(d_).sum(axis=0), then + p_initial), delta = max|d_ - d| (NaN wins),
+ * until delta <= eps (or max_iter sweeps when > 0).  Returns the sweep count.
+ */
+long long blas_order_forward_svf(const double* P, int S, int A, const double* p0, const uint8_t* term,
+                                 const double* pi, double eps, long long max_iter, double* d) {
+  if (S <= 0 || A <= 0 || (S & 3) > 1) return -1;
+  double* pa = malloc((size_t)A * S * S * sizeof(double));
+  double* x = malloc((size_t)S * sizeof(double));
+  double* y = malloc((size_t)A * S * sizeof(double));
+  double* dn = malloc((size_t)S * sizeof(double));
+  if (!pa || !x || !y || !dn) {
+    free(pa); free(x); free(y); free(dn);
+    return -2;
+  }
+  for (int a = 0; a < A; ++a)  /* maxent.py:98-102: the terminal rows cleared, then the slices */
+    for (int s = 0; s < S; ++s)
+      for (int t = 0; t < S; ++t) pa[((size_t)a * S + s) * S + t] = term[s] ? 0.0 : P[((size_t)s * S + t) * A + a];
+  for (int s = 0; s < S; ++s) d[s] = 0.0;
+  long long it = 0;
+  double delta = INFINITY;
+  while (delta > eps && (max_iter <= 0 || it < max_iter)) {
+    for (int a = 0; a < A; ++a) {
+      for (int s = 0; s < S; ++s) x[s] = pi[(size_t)s * A + a] * d[s];
+      blas_order_dgemv_cols(pa + (size_t)a * S * S, S, x, y + (size_t)a * S);
+    }
+    delta = 0.0;
+    for (int t = 0; t < S; ++t) {
+      double v = y[t];
+      for (int a = 1; a < A; ++a) v = v + y[(size_t)a * S + t];
+      dn[t] = p0[t] + v;
+      const double dd = fabs(dn[t] - d[t]);
+      if (dd != dd || (delta == delta && dd > delta)) delta = dd;
+    }
+    for (int t = 0; t < S; ++t) d[t] = dn[t];
+    ++it;
+  }
+  free(pa); free(x); free(y); free(dn);
+  return it;
+}

@@ -76,6 +76,11 @@ def _bwd_np(lib, m, a):
     return lib.irlmx_backward_maxent_numpy_order(m, a["exp_reward"], a["terminal"], a["p_action"], a["status"], NULL)
 
 
+def _fwd_np(lib, m, a):
+    return lib.irlmx_forward_svf_numpy_order(m, a["p_initial"], a["terminal"], a["p_action"], 1e-5, 0, a["svf"],
+                                             a["iterations"], a["status"], NULL)
+
+
 def _soft_np(lib, m, a):
     return lib.irlmx_soft_backward_numpy_order(m, a["reward"], a["terminal_reward"], 0.7, 1e-5, 0, a["p_action"],
                                                a["value"], a["iterations"], a["status"], NULL)
@@ -92,10 +97,12 @@ ENTRY = {
     "forward_svf": (2, _fwd, ("p_initial", "terminal", "p_action", "svf", "iterations", "status")),
     "soft_backward": (3, _soft, ("reward", "terminal_reward", "p_action", "iterations", "status")),
     "value_iteration": (4, _vi, ("reward", "value", "iterations", "status")),
+    "forward_svf_numpy_order": (2, _fwd_np, ("p_initial", "terminal", "p_action", "svf", "iterations", "status")),
     "soft_backward_numpy_order": (3, _soft_np, ("reward", "terminal_reward", "p_action", "iterations", "status")),
     "value_iteration_numpy_order": (4, _vi_np, ("reward", "value", "iterations", "status")),
 }
-NO_WORKSPACE = {"backward_maxent_numpy_order", "soft_backward_numpy_order", "value_iteration_numpy_order"}
+NO_WORKSPACE = {"backward_maxent_numpy_order", "forward_svf_numpy_order", "soft_backward_numpy_order",
+                "value_iteration_numpy_order"}
 ARGS = ("reward", "terminal", "p_action", "status", "p_initial", "svf", "iterations", "terminal_reward", "value",
         "exp_reward")
 
@@ -266,7 +273,7 @@ def test_numpy_order_sizes_einval(lib, S, W, H):
     """numpy's order is restated for S <= 4096 with S % 4 in {0, 1} only
     (oracle/blas_order.c): other sizes are rejected, not approximated."""
     m = model(S=S, W=W, H=H)
-    for call, op in ((_bwd_np, 1), (_soft_np, 3), (_vi_np, 4)):
+    for call, op in ((_bwd_np, 1), (_fwd_np, 2), (_soft_np, 3), (_vi_np, 4)):
         a = args_for(lib, model(), op)
         assert call(lib, ctypes.byref(m), a) == EINVAL
         assert "numpy's order is restated for S <= 4096" in err(lib), err(lib)

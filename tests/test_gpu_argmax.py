@@ -250,3 +250,64 @@ def test_value_iteration_numpy_order_bit_identical(dev):
             ref, kr = O.value_iteration_blas_order(P, r, 0.95, average=avg)
             v, k, _ = ops.value_iteration(mdp, r, 0.95, average=avg, numpy_order=True)
             assert int(k[0]) == kr and np.array_equal(v[0].cpu().numpy(), ref), (size, avg)
+
+
+def test_forward_numpy_order_bit_identical(dev):
+    """irlmx_forward_svf_numpy_order (maxent.py:105-114 in numpy's order): from
+    the reference's own policies, SVF and sweep counts bit-identical to the
+    reference's output for every maxent_small case -- the 11,858,933-sweep s8_unif
+    case included, which the tiled shapes may end a few sweeps early or late --,
+    config 1's svf1 / csvf1 and the non-grid tables; STENCIL5, ELL and DENSE
+    layouts (DENSE skips the 11.9M-sweep case)."""
+    import maxent as M
+    from irlmx import DeviceMDP, ops
+    z = load_golden("maxent_small")
+    for c in [str(n) for n in z["names"]]:
+        size = int(z[c + "__size"])
+        n = size * size
+        P = O.icy_gridworld_table(size, float(z[c + "__p_slip"]))
+        term = [int(t) for t in z[c + "__terminal"]]
+        tm = ops.terminal_mask(term, n, device=dev)
+        for layout in ("stencil", "ell", "dense"):
+            if layout == "dense" and int(z[c + "__k_f"]) > 100_000:
+                continue
+            mdp = DeviceMDP.from_dense(P, device=dev, layout=layout)
+            svf, k, st = ops.forward_svf(mdp, z[c + "__p0"], tm, z[c + "__pi"], numpy_order=True)
+            assert int(k[0]) == int(z[c + "__k_f"]), (c, layout, int(k[0]))
+            assert np.array_equal(svf[0].cpu().numpy(), z[c + "__svf"], equal_nan=True), (c, layout)
+    z1 = load_golden("config1")
+    P = z1["p_transition"]
+    assert np.array_equal(M.expected_svf_from_policy(P, z1["p_initial"], [24], z1["pi1"]), z1["svf1"])
+    assert np.array_equal(M.expected_svf_from_policy(P, z1["p_initial"], [24], z1["cpi1"]), z1["csvf1"])
+    assert np.array_equal(M.compute_expected_svf(P, z1["p_initial"], [24], np.ones(25)), z1["svf1"])
+    g = load_golden("generic")
+    for c in [str(n) for n in g["names"]]:
+        P = g[c + "__P"]
+        S = P.shape[0]
+        term = [int(t) for t in g[c + "__terminal"]]
+        for layout in ("ell", "dense"):
+            mdp = DeviceMDP.from_dense(P, device=dev, layout=layout)
+            svf, k, _ = ops.forward_svf(mdp, g[c + "__p0"], ops.terminal_mask(term, S, device=dev), g[c + "__pi"],
+                                        numpy_order=True)
+            assert int(k[0]) == int(g[c + "__k_f"]), (c, layout)
+            assert np.array_equal(svf[0].cpu().numpy(), g[c + "__svf"]), (c, layout)
+
+
+def test_config1_irl_bit_identical(dev):
+    """BASELINE config 1 (src/main.py) through the drop-in: maxent.irl's 375
+    steps reproduce the reference's recovered reward bit for bit (backward and
+    forward in numpy's order, the caller's numpy optimiser on the host), and
+    irl_causal its 419 steps within 1e-9 (the soft VI's exp / log are the
+    device's)."""
+    import maxent as M
+    from conftest import unpack_trajectories
+    z = load_golden("config1")
+    tjs = unpack_trajectories(z["traj_flat"], z["traj_lens"])
+    opt = O.ExpSga(lr=O.linear_decay(0.2))
+    r = M.irl(z["p_transition"], np.identity(25), [24], tjs, opt, O.Constant(1.0))
+    assert opt.k == int(z["irl_steps"]) == 375
+    assert np.array_equal(r, z["reward_maxent"]), np.max(np.abs(r - z["reward_maxent"]))
+    opt = O.ExpSga(lr=O.linear_decay(0.2))
+    r = M.irl_causal(z["p_transition"], np.identity(25), [24], tjs, opt, O.Constant(1.0), 0.7)
+    assert opt.k == int(z["causal_steps"]) == 419
+    assert np.max(np.abs(r - z["reward_causal"])) <= 1e-9
