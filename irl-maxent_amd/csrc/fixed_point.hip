@@ -700,6 +700,162 @@ __global__ void __launch_bounds__(1024) fwd_numpy_order_kernel(NpFwdArgs a) {
   }
 }
 
+// The same forward for a STENCIL5 model with TPT targets per thread (512
+// threads; S <= 1024, A <= 4): each thread keeps its targets' sources, the
+// processing order of np_col_dot and every P[s, t, a] and pi[s, a] it
+// multiplies in registers, so a sweep is five LDS reads per target and the
+// chains -- no global load, no index arithmetic (the general kernel re-derives
+// them every sweep, ~15 us per sweep at 64 states).
+constexpr int kNpCachedThreads = 512;
+constexpr int kNpCachedMaxStates = 2 * kNpCachedThreads;
+constexpr int kNpCachedMaxActions = 4;
+template <int TPT>
+__global__ void __launch_bounds__(kNpCachedThreads) fwd_numpy_order_cached_kernel(NpFwdArgs a) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  const Model& m = a.m;
+  const int S = m.S, A = m.A, n4 = S & ~3;
+  const int b = blockIdx.x, tid = threadIdx.x, nt = blockDim.x;
+  double* buf[2] = {(double*)smem, (double*)smem + S};
+  unsigned long long* slot = (unsigned long long*)(buf[1] + S);
+  int* bad = (int*)(slot + 3);
+  const double* pi = a.pi + (size_t)b * S * A;
+  const uint8_t* term = a.term + (size_t)b * S;
+  // per target j: entries in processing order; kind: 0 chain continues, 1 chain
+  // starts (the previous chain's sum added first), 2 tail source (rounded
+  // product added), 3 tail output (one fma chain).  (Every array is indexed by
+  // compile-time constants only: registers, not scratch.)
+  int src[TPT][kStencilK], kind[TPT][kStencilK], n[TPT];
+  double val[TPT][kNpCachedMaxActions][kStencilK], pw[TPT][kNpCachedMaxActions][kStencilK], p0t[TPT];
+  constexpr int order[kStencilK] = {4, 2, 0, 1, 3};  // candidate sources t - W, t - 1, t, t + 1, t + W
+#pragma unroll
+  for (int j = 0; j < TPT; ++j) {
+    const int t = tid + j * nt;
+    n[j] = 0;
+    p0t[j] = 0.0;
+#pragma unroll
+    for (int p = 0; p < kStencilK; ++p) {
+      src[j][p] = 0;
+      kind[j][p] = 0;
+#pragma unroll
+      for (int act = 0; act < kNpCachedMaxActions; ++act) { val[j][act][p] = 0.0; pw[j][act][p] = 0.0; }
+    }
+    if (t >= S) continue;
+    p0t[j] = a.p0[(size_t)b * S + t];
+    int cs[kStencilK], key[kStencilK];
+    bool ok[kStencilK];
+#pragma unroll
+    for (int i = 0; i < kStencilK; ++i) {
+      ok[i] = stencil_valid(t, order[i], m.W, m.H);
+      cs[i] = stencil_nbr(t, order[i], m.W, m.H);
+      ok[i] = ok[i] && !term[cs[i]];  // P' rows of terminal states are zero (maxent.py:99)
+      // processing key: group, then source order 4g + 1, 4g, 4g + 2, 4g + 3; tail sources after
+      const int q = cs[i] & 3;
+      key[i] = t >= n4 ? cs[i] : (cs[i] < n4 ? 4 * (cs[i] >> 2) + (q == 1 ? 0 : q == 0 ? 1 : q) : 4 * S + cs[i]);
+    }
+#pragma unroll
+    for (int i = 0; i < kStencilK; ++i) {
+      if (!ok[i]) continue;
+      int pos = 0;
+      bool first = true;  // lowest key of its group among the valid sources
+#pragma unroll
+      for (int q = 0; q < kStencilK; ++q) {
+        pos += (ok[q] && key[q] < key[i]) ? 1 : 0;
+        first = first && !(ok[q] && key[q] < key[i] && (cs[q] >> 2) == (cs[i] >> 2));
+      }
+      const int kd = t >= n4 ? 3 : (cs[i] >= n4 ? 2 : (first ? 1 : 0));
+#pragma unroll
+      for (int p = 0; p < kStencilK; ++p)
+        if (pos == p) {
+          src[j][p] = cs[i];
+          kind[j][p] = kd;
+#pragma unroll
+          for (int act = 0; act < kNpCachedMaxActions; ++act) {
+            val[j][act][p] = act < A ? row_val(m, b, act, stencil_opposite(order[i]), cs[i]) : 0.0;
+            pw[j][act][p] = act < A ? pi[(size_t)cs[i] * A + act] : 0.0;
+          }
+        }
+      ++n[j];
+    }
+  }
+  bool nf = false;
+  for (int s = tid; s < S; s += nt) {
+    buf[0][s] = 0.0;  // maxent.py:105
+    for (int act = 0; act < A; ++act) nf |= !isfinite(pi[(size_t)s * A + act]);
+  }
+  if (tid < 3) slot[tid] = 0ull;
+  if (tid < 2) bad[tid] = 0;
+  __syncthreads();
+  if (nf) bad[1] = 1;
+  __syncthreads();
+  long long it = 0;
+  int r3 = 0;
+  double delta = 0.0;
+  for (;;) {
+    const double* d = buf[it & 1];
+    double* dn = buf[(it & 1) ^ 1];
+    const bool poisoned = bad[(it & 1) ^ 1] != 0;
+    unsigned long long mx = 0ull;
+    bool nfo = false;
+#pragma unroll
+    for (int j = 0; j < TPT; ++j) {
+      const int t = tid + j * nt;
+      if (t >= S) continue;
+      double dv[kStencilK];
+#pragma unroll
+      for (int i = 0; i < kStencilK; ++i) dv[i] = i < n[j] ? d[src[j][i]] : 0.0;
+      double v = 0.0;
+#pragma unroll
+      for (int act = 0; act < kNpCachedMaxActions; ++act) {
+        if (act >= A) break;
+        double out = 0.0, c = 0.0;
+        bool open = false;
+#pragma unroll
+        for (int i = 0; i < kStencilK; ++i) {
+          if (i >= n[j]) break;
+          const double x = __dmul_rn(pw[j][act][i], dv[i]);  // maxent.py:109
+          const int kd = kind[j][i];
+          if (kd == 3) {
+            out = fma(val[j][act][i], x, out);
+          } else if (kd == 2) {
+            if (open) { out = __dadd_rn(out, c); open = false; }
+            out = __dadd_rn(out, __dmul_rn(val[j][act][i], x));
+          } else {
+            if (kd == 1) {
+              if (open) out = __dadd_rn(out, c);
+              c = 0.0;
+              open = true;
+            }
+            c = fma(val[j][act][i], x, c);
+          }
+        }
+        if (open) out = __dadd_rn(out, c);
+        const double y = poisoned ? kNaN : out;
+        v = act == 0 ? y : __dadd_rn(v, y);  // np.array(d_).sum(axis=0)
+      }
+      const double nv = __dadd_rn(p0t[j], v);  // maxent.py:110
+      dn[t] = nv;
+      nfo |= !isfinite(nv);
+      const unsigned long long dd = abs_bits(nv - d[t]);
+      mx = dd > mx ? dd : mx;
+    }
+    if (nfo) bad[it & 1] = 1;
+    mx = wave_max_u64(mx);
+    if ((tid & (kWave - 1)) == 0 && mx) atomicMax(&slot[r3], mx);
+    if (tid == 0) slot[r3 == 2 ? 0 : r3 + 1] = 0ull;
+    __syncthreads();
+    delta = bits_double(slot[r3]);
+    r3 = r3 == 2 ? 0 : r3 + 1;
+    ++it;
+    if (!(delta > a.eps)) break;  // maxent.py:108
+    if (a.max_iter > 0 && it >= a.max_iter) break;
+  }
+  for (int t = tid; t < S; t += nt) a.svf[(size_t)b * S + t] = buf[it & 1][t];
+  if (tid == 0) {
+    a.iters[b] = it;
+    a.status[b] = finish_status(delta, a.eps);
+  }
+}
+
 template <int LAYOUT>
 __global__ void __launch_bounds__(1024) bwd_numpy_order_kernel(NpArgs a) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
@@ -2369,14 +2525,18 @@ extern "C" int irlmx_forward_svf_numpy_order(const irlmx_mdp* mdp, const double*
     return IRLMX_EINVAL;
   }
   NpFwdArgs a{m, p_initial, terminal, p_action, eps, (long long)max_iter, svf, iterations, status};
-  void (*k)(NpFwdArgs) = m.stencil ? fwd_numpy_order_kernel<IRLMX_LAYOUT_STENCIL5>
-                                   : (m.dense ? fwd_numpy_order_kernel<IRLMX_LAYOUT_DENSE>
-                                              : fwd_numpy_order_kernel<IRLMX_LAYOUT_ELL>);
+  const bool cached = m.stencil && m.S <= kNpCachedMaxStates && m.A <= kNpCachedMaxActions;
+  void (*k)(NpFwdArgs) = cached ? (m.S <= kNpCachedThreads ? fwd_numpy_order_cached_kernel<1>
+                                                           : fwd_numpy_order_cached_kernel<2>)
+                                : m.stencil ? fwd_numpy_order_kernel<IRLMX_LAYOUT_STENCIL5>
+                                            : (m.dense ? fwd_numpy_order_kernel<IRLMX_LAYOUT_DENSE>
+                                                       : fwd_numpy_order_kernel<IRLMX_LAYOUT_ELL>);
   const size_t lds = 2 * (size_t)m.S * sizeof(double) + 3 * sizeof(unsigned long long) + 2 * sizeof(int);
   hipError_t e = hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
   if (e != hipSuccess) return hip_fail(e, "hipFuncSetAttribute");
-  hipLaunchKernelGGL(k, dim3(m.B), dim3(m.S >= 1024 ? 1024 : ((m.S + kWave - 1) / kWave) * kWave), lds,
-                     (hipStream_t)stream, a);
+  const int nthr = cached ? std::min(kNpCachedThreads, ((m.S + kWave - 1) / kWave) * kWave)
+                          : (m.S >= 1024 ? 1024 : ((m.S + kWave - 1) / kWave) * kWave);
+  hipLaunchKernelGGL(k, dim3(m.B), dim3(nthr), lds, (hipStream_t)stream, a);
   e = hipGetLastError();
   return e == hipSuccess ? 0 : hip_fail(e, "forward_svf_numpy_order");
 }

@@ -7,7 +7,7 @@
 set -e
 TAG=${1:-r01}
 shift || true
-ARGS=${@:-"--steps 2 --warmup 1 --no-cpu-baseline --no-config1 --first-steps 0"}
+ARGS=${@:-"--steps 2 --warmup 1 --no-cpu-baseline --no-config1 --first-steps 0 --no-full-run"}
 ROOT=$(pwd)
 OUT=$ROOT/gpurun_out/prof_$TAG
 mkdir -p $OUT
