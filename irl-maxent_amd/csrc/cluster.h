@@ -18,7 +18,7 @@ constexpr int kSptMaxQuadFwd = 12;  // forward with column quads (register budge
 // rows instead of 4 halve the exchanges)
 constexpr int kSptMaxQuadBwd = 16;
 constexpr int kTMax = 16;          // max sweeps per block (= max ghost rows)
-constexpr int kSoloBwdT = 64;      // backward sweeps per block of a solo tile (no ghost rows)
+constexpr int kSoloBwdT = 256;     // backward sweeps per block of a solo tile (no ghost rows)
 constexpr int kRescaleEvery = 4;   // backward: max blocks between rescales
 constexpr size_t kMaxLdsBytes = 160 * 1024;  // LDS per CU (one workgroup per CU)
 constexpr int kModeFwd = 0;

@@ -952,8 +952,9 @@ bool cluster_plan(int W, int H, int B, int mode, ClusterPlan* out) {
       // A solo tile has no ghost rows, so its block length is free: the backward
       // runs blocks of kSoloBwdT sweeps (IRLMX_SOLO_T; the growth cap still
       // bounds it), amortising the ~1.9k cycles of per-block bookkeeping
-      // (rescale test, summary, register refresh) over 4x more sweeps.  (The
-      // forward's per-sweep convergence bits hold 16 sweeps per block.)
+      // (rescale test, summary, register refresh) over 16x more sweeps: config 2
+      // backward 3.42 -> 2.77 ms.  (The forward's per-sweep convergence bits
+      // hold 16 sweeps per block.)
       const int T = (solo && mode == kModeBwd) ? std::max(1, env_int("IRLMX_SOLO_T", kSoloBwdT)) : G;
       const double cost = nl * (std::max((mode == kModeFwd ? 165.0 : 110.0) * spt, 850.0) * T + xchg) / T;
       if (cost < best - 1e-9) {
