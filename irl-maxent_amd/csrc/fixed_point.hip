@@ -856,6 +856,93 @@ __global__ void __launch_bounds__(kNpCachedThreads) fwd_numpy_order_cached_kerne
   }
 }
 
+// The numpy-order backward for a STENCIL5 model with TPT states per thread
+// (512 threads; S <= 1024, A <= 4): each thread keeps its states' columns, their
+// dgemv lanes (column % 4; the last column S - 1 of an S % 4 == 1 grid fused on
+// after the lane sum) and every P[s, c, a] in registers, so a sweep is five LDS
+// reads per state and the lane chains (np_row_dot's arithmetic exactly; the
+// general kernel re-derives indices and re-loads P every sweep).
+template <int TPT>
+__global__ void __launch_bounds__(kNpCachedThreads) bwd_numpy_order_cached_kernel(NpArgs a) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  const Model& m = a.m;
+  const int S = m.S, A = m.A, m1 = S & ~3;
+  const int b = blockIdx.x, tid = threadIdx.x, nt = blockDim.x;
+  double* zbuf[2] = {(double*)smem, (double*)smem + S};
+  int* bad = (int*)(zbuf[1] + S);
+  const double* er = a.er + (size_t)b * S;
+  double* pi = a.pi + (size_t)b * S * A;
+  constexpr int order[kStencilK] = {4, 2, 0, 1, 3};  // ascending columns: -y, -x, self, +x, +y
+  // per state j, candidate column i (static indices only): column, lane (4 = the tail column, -1 = absent)
+  int col[TPT][kStencilK], lane[TPT][kStencilK];
+  double val[TPT][kNpCachedMaxActions][kStencilK], ers[TPT];
+#pragma unroll
+  for (int j = 0; j < TPT; ++j) {
+    const int s = tid + j * nt;
+    ers[j] = s < S ? er[s] : 0.0;
+#pragma unroll
+    for (int i = 0; i < kStencilK; ++i) {
+      const bool ok = s < S && stencil_valid(s, order[i], m.W, m.H);
+      col[j][i] = ok ? stencil_nbr(s, order[i], m.W, m.H) : 0;
+      lane[j][i] = ok ? (col[j][i] < m1 ? (col[j][i] & 3) : 4) : -1;
+#pragma unroll
+      for (int act = 0; act < kNpCachedMaxActions; ++act)
+        val[j][act][i] = (ok && act < A) ? row_val(m, b, act, order[i], s) : 0.0;
+    }
+  }
+  for (int s = tid; s < S; s += nt) zbuf[0][s] = a.term[(size_t)b * S + s] ? 1.0 : 0.0;  // maxent.py:146-147
+  if (tid < 2) bad[tid] = 0;
+  __syncthreads();
+  const long long n = 2LL * S;  // maxent.py:154
+  for (long long it = 0; it < n; ++it) {
+    const double* zin = zbuf[it & 1];
+    double* zout = zbuf[(it & 1) ^ 1];
+    if (it > 0 && bad[(it - 1) & 1]) {  // the reference's overflow: NaN from here on (bwd_numpy_order_kernel)
+      for (int s = tid; s < S; s += nt)
+        for (int act = 0; act < A; ++act) pi[(size_t)s * A + act] = kNaN;
+      if (tid == 0) a.status[b] = IRLMX_OK;
+      return;
+    }
+    bool nf = false;
+#pragma unroll
+    for (int j = 0; j < TPT; ++j) {
+      const int s = tid + j * nt;
+      if (s >= S) continue;
+      const bool fused = s < m1;  // dgemv_kernel_4x4 rows; the last row of an S % 4 == 1 grid: 4x1
+      double x[kStencilK];
+#pragma unroll
+      for (int i = 0; i < kStencilK; ++i) x[i] = lane[j][i] >= 0 ? zin[col[j][i]] : 0.0;
+      double z = 0.0;
+#pragma unroll
+      for (int act = 0; act < kNpCachedMaxActions; ++act) {
+        if (act >= A) break;
+        double l[4] = {0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+        for (int q = 0; q < 4; ++q)
+#pragma unroll
+          for (int i = 0; i < kStencilK; ++i)  // ascending columns within a lane
+            if (lane[j][i] == q)
+              l[q] = fused ? fma(val[j][act][i], x[i], l[q]) : __dadd_rn(l[q], __dmul_rn(val[j][act][i], x[i]));
+        double y = __dadd_rn(0.0, __dadd_rn(__dadd_rn(l[0], l[2]), __dadd_rn(l[1], l[3])));
+#pragma unroll
+        for (int i = 0; i < kStencilK; ++i)
+          if (lane[j][i] == 4) y = fma(val[j][act][i], x[i], y);
+        const double za = __dmul_rn(ers[j], y);  // maxent.py:155
+        z = act == 0 ? za : __dadd_rn(z, za);    // maxent.py:156
+        if (it == n - 1) pi[(size_t)s * A + act] = za;
+      }
+      zout[s] = z;
+      nf |= !isfinite(z);
+    }
+    if (nf) bad[it & 1] = 1;
+    __syncthreads();
+  }
+  const double* zs = zbuf[n & 1];
+  for (int s = tid; s < S; s += nt)
+    for (int act = 0; act < A; ++act) pi[(size_t)s * A + act] = pi[(size_t)s * A + act] / zs[s];  // maxent.py:159
+  if (tid == 0) a.status[b] = IRLMX_OK;
+}
+
 template <int LAYOUT>
 __global__ void __launch_bounds__(1024) bwd_numpy_order_kernel(NpArgs a) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
@@ -876,11 +963,19 @@ __global__ void __launch_bounds__(1024) bwd_numpy_order_kernel(NpArgs a) {
     // a non-finite zs meets a zero entry of every dense row (0 * inf): the
     // reference's next dots are all NaN (a DENSE row visits every column itself)
     const bool poisoned = LAYOUT != IRLMX_LAYOUT_DENSE && it > 0 && bad[(it - 1) & 1];
+    if (poisoned) {
+      // from here every dot, za and zs is NaN (the overflow the reference hits at
+      // about 13 x 13 and unit reward): the policy is NaN, no need to sweep on
+      for (int s = tid; s < S; s += nt)
+        for (int act = 0; act < A; ++act) pi[(size_t)s * A + act] = kNaN;
+      if (tid == 0) a.status[b] = IRLMX_OK;
+      return;
+    }
     bool nf = false;
     for (int s = tid; s < S; s += nt) {
       double z = 0.0;
       for (int act = 0; act < A; ++act) {
-        const double dot = poisoned ? kNaN : np_row_dot<LAYOUT>(m, b, act, s, zin);
+        const double dot = np_row_dot<LAYOUT>(m, b, act, s, zin);
         const double za = __dmul_rn(er[s], dot);                 // maxent.py:155
         z = act == 0 ? za : __dadd_rn(z, za);                    // maxent.py:156
         if (it == n - 1) pi[(size_t)s * A + act] = za;
@@ -2398,13 +2493,18 @@ extern "C" int irlmx_backward_maxent_numpy_order(const irlmx_mdp* mdp, const dou
   }
   hipStream_t st = (hipStream_t)stream;
   NpArgs a{m, exp_reward, terminal, p_action, status};
-  void (*fn)(NpArgs) = m.stencil ? bwd_numpy_order_kernel<IRLMX_LAYOUT_STENCIL5>
-                                 : (m.dense ? bwd_numpy_order_kernel<IRLMX_LAYOUT_DENSE>
-                                            : bwd_numpy_order_kernel<IRLMX_LAYOUT_ELL>);
+  const bool cached = m.stencil && m.S <= kNpCachedMaxStates && m.A <= kNpCachedMaxActions;
+  void (*fn)(NpArgs) = cached ? (m.S <= kNpCachedThreads ? bwd_numpy_order_cached_kernel<1>
+                                                         : bwd_numpy_order_cached_kernel<2>)
+                              : m.stencil ? bwd_numpy_order_kernel<IRLMX_LAYOUT_STENCIL5>
+                                          : (m.dense ? bwd_numpy_order_kernel<IRLMX_LAYOUT_DENSE>
+                                                     : bwd_numpy_order_kernel<IRLMX_LAYOUT_ELL>);
   const size_t lds = 2 * (size_t)m.S * sizeof(double) + 2 * sizeof(int);
   hipError_t e = hipFuncSetAttribute((const void*)fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
   if (e != hipSuccess) return hip_fail(e, "hipFuncSetAttribute");
-  hipLaunchKernelGGL(fn, dim3(m.B), dim3(m.S >= 1024 ? 1024 : ((m.S + kWave - 1) / kWave) * kWave), lds, st, a);
+  const int nthr = cached ? std::min(kNpCachedThreads, ((m.S + kWave - 1) / kWave) * kWave)
+                          : (m.S >= 1024 ? 1024 : ((m.S + kWave - 1) / kWave) * kWave);
+  hipLaunchKernelGGL(fn, dim3(m.B), dim3(nthr), lds, st, a);
   e = hipGetLastError();
   return e == hipSuccess ? 0 : hip_fail(e, "backward_maxent_numpy_order");
 }

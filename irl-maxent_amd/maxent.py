@@ -120,7 +120,9 @@ def _forward(mdp, p_initial, term, pi, eps):
 
 def _backward(mdp, reward, term):
     """The backward policy on the device: numpy's order where the model allows it
-    (bit-identical to the reference), the rescaled pass where that overflows."""
+    (bit-identical to the reference), the rescaled pass where that overflows
+    (the numpy-order kernel stops at the overflow, so the detour costs the sweeps
+    up to it: a few hundred at unit reward)."""
     reward = np.asarray(reward.cpu().numpy() if torch.is_tensor(reward) else reward, dtype=np.float64)
     if _np_order(mdp):
         pi = ops.backward_maxent_numpy_order(mdp, np.exp(reward), term)   # er = np.exp(reward), maxent.py:142

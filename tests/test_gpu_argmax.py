@@ -333,3 +333,21 @@ def test_forward_numpy_order_two_targets_per_lane(dev, size):
     svf, k, _ = ops.forward_svf(mdp, p0, ops.terminal_mask(term, n, device=dev), pi, max_iter=200, numpy_order=True)
     assert int(k[0]) == kr == 200
     assert np.array_equal(svf[0].cpu().numpy(), ref)
+
+
+@pytest.mark.parametrize("size", [16, 23])
+def test_backward_numpy_order_cached_against_restatement(dev, size):
+    """The register-cached numpy-order backward (one state per lane at 16x16,
+    two at 23x23 = 529 states, S % 4 = 1: the last row's rounded-product lanes
+    and the fused last column) against the C restatement of numpy's order, with
+    rewards near -ln 4 so that the 2 S sweeps neither overflow nor underflow:
+    bit for bit."""
+    from irlmx import DeviceMDP, ops
+    n = size * size
+    r = -np.log(4.0) + np.random.default_rng(size).uniform(-0.05, 0.05, n)
+    P = O.icy_gridworld_table(size, 0.2)
+    ref = O.backward_maxent_blas_order(P, [n - 1], r)
+    assert np.isfinite(ref).all()
+    mdp = DeviceMDP.icy_gridworld(size, 0.2, device=dev)
+    pi = ops.backward_maxent_numpy_order(mdp, np.exp(r), ops.terminal_mask([n - 1], n, device=dev))
+    assert np.array_equal(pi[0].cpu().numpy(), ref)
