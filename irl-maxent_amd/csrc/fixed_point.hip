@@ -856,12 +856,58 @@ __global__ void __launch_bounds__(kNpCachedThreads) fwd_numpy_order_cached_kerne
   }
 }
 
+// A thread's stencil rows in registers for the numpy-order kernels (TPT states
+// per thread, A <= 4): per state j and candidate column i (ascending: -y, -x,
+// self, +x, +y) the column, its dgemv lane (column % 4; 4 = the last column
+// S - 1 of an S % 4 == 1 grid, fused on after the lane sum; -1 = off-grid) and
+// P[s, c, a] -- np_row_dot's arithmetic without re-deriving indices or
+// re-loading P every sweep.  Static indices only: registers, not scratch.
+template <int TPT>
+struct NpStencilRows {
+  int col[TPT][kStencilK], lane[TPT][kStencilK];
+  double val[TPT][kNpCachedMaxActions][kStencilK];
+
+  __device__ void load(const Model& m, int b, int tid, int nt) {
+    constexpr int order[kStencilK] = {4, 2, 0, 1, 3};
+    const int S = m.S, m1 = S & ~3;
+#pragma unroll
+    for (int j = 0; j < TPT; ++j) {
+      const int s = tid + j * nt;
+#pragma unroll
+      for (int i = 0; i < kStencilK; ++i) {
+        const bool ok = s < S && stencil_valid(s, order[i], m.W, m.H);
+        col[j][i] = ok ? stencil_nbr(s, order[i], m.W, m.H) : 0;
+        lane[j][i] = ok ? (col[j][i] < m1 ? (col[j][i] & 3) : 4) : -1;
+#pragma unroll
+        for (int act = 0; act < kNpCachedMaxActions; ++act)
+          val[j][act][i] = (ok && act < m.A) ? row_val(m, b, act, order[i], s) : 0.0;
+      }
+    }
+  }
+  // the vector at state j's columns
+  __device__ void gather(int j, const double* v, double (&x)[kStencilK]) const {
+#pragma unroll
+    for (int i = 0; i < kStencilK; ++i) x[i] = lane[j][i] >= 0 ? v[col[j][i]] : 0.0;
+  }
+  // p[act][s, :] . v in OpenBLAS dgemv_t order (fused: rows s < S & ~3)
+  __device__ double dot(int j, int act, bool fused, const double (&x)[kStencilK]) const {
+    double l[4] = {0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+    for (int q = 0; q < 4; ++q)
+#pragma unroll
+      for (int i = 0; i < kStencilK; ++i)  // ascending columns within a lane
+        if (lane[j][i] == q)
+          l[q] = fused ? fma(val[j][act][i], x[i], l[q]) : __dadd_rn(l[q], __dmul_rn(val[j][act][i], x[i]));
+    double y = __dadd_rn(0.0, __dadd_rn(__dadd_rn(l[0], l[2]), __dadd_rn(l[1], l[3])));
+#pragma unroll
+    for (int i = 0; i < kStencilK; ++i)
+      if (lane[j][i] == 4) y = fma(val[j][act][i], x[i], y);
+    return y;
+  }
+};
+
 // The numpy-order backward for a STENCIL5 model with TPT states per thread
-// (512 threads; S <= 1024, A <= 4): each thread keeps its states' columns, their
-// dgemv lanes (column % 4; the last column S - 1 of an S % 4 == 1 grid fused on
-// after the lane sum) and every P[s, c, a] in registers, so a sweep is five LDS
-// reads per state and the lane chains (np_row_dot's arithmetic exactly; the
-// general kernel re-derives indices and re-loads P every sweep).
+// (512 threads; S <= 1024, A <= 4), the rows in registers (NpStencilRows).
 template <int TPT>
 __global__ void __launch_bounds__(kNpCachedThreads) bwd_numpy_order_cached_kernel(NpArgs a) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
@@ -872,24 +918,11 @@ __global__ void __launch_bounds__(kNpCachedThreads) bwd_numpy_order_cached_kerne
   int* bad = (int*)(zbuf[1] + S);
   const double* er = a.er + (size_t)b * S;
   double* pi = a.pi + (size_t)b * S * A;
-  constexpr int order[kStencilK] = {4, 2, 0, 1, 3};  // ascending columns: -y, -x, self, +x, +y
-  // per state j, candidate column i (static indices only): column, lane (4 = the tail column, -1 = absent)
-  int col[TPT][kStencilK], lane[TPT][kStencilK];
-  double val[TPT][kNpCachedMaxActions][kStencilK], ers[TPT];
+  NpStencilRows<TPT> rows;
+  rows.load(m, b, tid, nt);
+  double ers[TPT];
 #pragma unroll
-  for (int j = 0; j < TPT; ++j) {
-    const int s = tid + j * nt;
-    ers[j] = s < S ? er[s] : 0.0;
-#pragma unroll
-    for (int i = 0; i < kStencilK; ++i) {
-      const bool ok = s < S && stencil_valid(s, order[i], m.W, m.H);
-      col[j][i] = ok ? stencil_nbr(s, order[i], m.W, m.H) : 0;
-      lane[j][i] = ok ? (col[j][i] < m1 ? (col[j][i] & 3) : 4) : -1;
-#pragma unroll
-      for (int act = 0; act < kNpCachedMaxActions; ++act)
-        val[j][act][i] = (ok && act < A) ? row_val(m, b, act, order[i], s) : 0.0;
-    }
-  }
+  for (int j = 0; j < TPT; ++j) ers[j] = tid + j * nt < S ? er[tid + j * nt] : 0.0;
   for (int s = tid; s < S; s += nt) zbuf[0][s] = a.term[(size_t)b * S + s] ? 1.0 : 0.0;  // maxent.py:146-147
   if (tid < 2) bad[tid] = 0;
   __syncthreads();
@@ -908,27 +941,14 @@ __global__ void __launch_bounds__(kNpCachedThreads) bwd_numpy_order_cached_kerne
     for (int j = 0; j < TPT; ++j) {
       const int s = tid + j * nt;
       if (s >= S) continue;
-      const bool fused = s < m1;  // dgemv_kernel_4x4 rows; the last row of an S % 4 == 1 grid: 4x1
       double x[kStencilK];
-#pragma unroll
-      for (int i = 0; i < kStencilK; ++i) x[i] = lane[j][i] >= 0 ? zin[col[j][i]] : 0.0;
+      rows.gather(j, zin, x);
       double z = 0.0;
 #pragma unroll
       for (int act = 0; act < kNpCachedMaxActions; ++act) {
         if (act >= A) break;
-        double l[4] = {0.0, 0.0, 0.0, 0.0};
-#pragma unroll
-        for (int q = 0; q < 4; ++q)
-#pragma unroll
-          for (int i = 0; i < kStencilK; ++i)  // ascending columns within a lane
-            if (lane[j][i] == q)
-              l[q] = fused ? fma(val[j][act][i], x[i], l[q]) : __dadd_rn(l[q], __dmul_rn(val[j][act][i], x[i]));
-        double y = __dadd_rn(0.0, __dadd_rn(__dadd_rn(l[0], l[2]), __dadd_rn(l[1], l[3])));
-#pragma unroll
-        for (int i = 0; i < kStencilK; ++i)
-          if (lane[j][i] == 4) y = fma(val[j][act][i], x[i], y);
-        const double za = __dmul_rn(ers[j], y);  // maxent.py:155
-        z = act == 0 ? za : __dadd_rn(z, za);    // maxent.py:156
+        const double za = __dmul_rn(ers[j], rows.dot(j, act, s < m1, x));  // maxent.py:155
+        z = act == 0 ? za : __dadd_rn(z, za);                               // maxent.py:156
         if (it == n - 1) pi[(size_t)s * A + act] = za;
       }
       zout[s] = z;
@@ -1193,6 +1213,94 @@ __global__ void __launch_bounds__(1024) bellman_numpy_order_kernel(SoftArgs a) {
         const double q = __dadd_rn(rw[s], __dmul_rn(a.discount, np_row_dot<LAYOUT>(m, b, act, s, vold)));
         a.pi[((size_t)b * S + s) * A + act] = exp(q - vnew[s]);  // maxent.py:341
       }
+  }
+  if (tid == 0) {
+    if (a.iters) a.iters[b] = it;
+    a.status[b] = finish_status(delta, a.eps);
+  }
+}
+
+// Soft VI / VI in numpy's order for a STENCIL5 model with TPT states per
+// thread (512 threads; S <= 1024, A <= 4), the rows in registers (NpStencilRows).
+template <bool SOFT, int TPT>
+__global__ void __launch_bounds__(kNpCachedThreads) bellman_numpy_order_cached_kernel(SoftArgs a) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  const Model& m = a.m;
+  const int S = m.S, A = m.A, m1 = S & ~3;
+  const int b = blockIdx.x, tid = threadIdx.x, nt = blockDim.x;
+  double* buf[2] = {(double*)smem, (double*)smem + S};
+  unsigned long long* slot = (unsigned long long*)(buf[1] + S);
+  const double v0 = SOFT ? -1e200 : 0.0;  // maxent.py:323 / solver.py:29
+  NpStencilRows<TPT> rows;
+  rows.load(m, b, tid, nt);
+  double rr[TPT], ph[TPT];
+#pragma unroll
+  for (int j = 0; j < TPT; ++j) {
+    const int s = tid + j * nt;
+    rr[j] = s < S ? a.reward[(size_t)b * S + s] : 0.0;
+    ph[j] = (SOFT && s < S) ? a.phi[(size_t)b * S + s] : 0.0;
+  }
+  for (int s = tid; s < S; s += nt) buf[0][s] = v0;
+  if (tid < 3) slot[tid] = 0ull;
+  __syncthreads();
+  long long it = 0;
+  int r3 = 0;
+  double delta = 0.0;
+  for (;;) {
+    const double* vin = buf[it & 1];
+    double* vout = buf[(it & 1) ^ 1];
+    unsigned long long mx = 0ull;
+#pragma unroll
+    for (int j = 0; j < TPT; ++j) {
+      const int s = tid + j * nt;
+      if (s >= S) continue;
+      double x[kStencilK];
+      rows.gather(j, vin, x);
+      double v = SOFT ? ph[j] : 0.0;
+#pragma unroll
+      for (int act = 0; act < kNpCachedMaxActions; ++act) {
+        if (act >= A) break;
+        const double dot = rows.dot(j, act, s < m1, x);
+        if (SOFT) {
+          v = softmax2(v, __dadd_rn(rr[j], __dmul_rn(a.discount, dot)));  // maxent.py:329-333
+        } else {
+          const double q = __dmul_rn(a.discount, dot);  // solver.py:44
+          if (a.average) v = act == 0 ? q : __dadd_rn(v, q);
+          else v = act == 0 ? q : ((v != v || q <= v) ? v : q);
+        }
+      }
+      if (!SOFT) v = __dadd_rn(rr[j], a.average ? v / (double)A : v);  // solver.py:47 / :99
+      vout[s] = v;
+      const unsigned long long d = abs_bits(v - vin[s]);
+      mx = d > mx ? d : mx;
+    }
+    mx = wave_max_u64(mx);
+    if ((tid & (kWave - 1)) == 0 && mx) atomicMax(&slot[r3], mx);
+    if (tid == 0) slot[r3 == 2 ? 0 : r3 + 1] = 0ull;
+    __syncthreads();
+    delta = bits_double(slot[r3]);
+    r3 = r3 == 2 ? 0 : r3 + 1;
+    ++it;
+    if (!(delta > a.eps)) break;
+    if (a.max_iter > 0 && it >= a.max_iter) break;
+  }
+  const double* vold = buf[(it & 1) ^ 1];  // input of the last sweep
+  const double* vnew = buf[it & 1];
+#pragma unroll
+  for (int j = 0; j < TPT; ++j) {
+    const int s = tid + j * nt;
+    if (s >= S) continue;
+    if (a.value) a.value[(size_t)b * S + s] = vnew[s];
+    if (SOFT) {
+      double x[kStencilK];
+      rows.gather(j, vold, x);
+#pragma unroll
+      for (int act = 0; act < kNpCachedMaxActions; ++act) {
+        if (act >= A) break;
+        const double q = __dadd_rn(rr[j], __dmul_rn(a.discount, rows.dot(j, act, s < m1, x)));
+        a.pi[((size_t)b * S + s) * A + act] = exp(q - vnew[s]);  // maxent.py:341
+      }
+    }
   }
   if (tid == 0) {
     if (a.iters) a.iters[b] = it;
@@ -2658,7 +2766,12 @@ static int bellman_numpy_order(const irlmx_mdp* mdp, const double* reward, const
   }
   SoftArgs a{m, reward, phi, discount, eps, (long long)max_iter, average, p_action, value, iterations, status};
   void (*k)(SoftArgs) = nullptr;
-  if (m.stencil) k = soft ? bellman_numpy_order_kernel<true, IRLMX_LAYOUT_STENCIL5>
+  const bool cached = m.stencil && m.S <= kNpCachedMaxStates && m.A <= kNpCachedMaxActions;
+  if (cached) {
+    if (m.S <= kNpCachedThreads) k = soft ? bellman_numpy_order_cached_kernel<true, 1>
+                                          : bellman_numpy_order_cached_kernel<false, 1>;
+    else k = soft ? bellman_numpy_order_cached_kernel<true, 2> : bellman_numpy_order_cached_kernel<false, 2>;
+  } else if (m.stencil) k = soft ? bellman_numpy_order_kernel<true, IRLMX_LAYOUT_STENCIL5>
                           : bellman_numpy_order_kernel<false, IRLMX_LAYOUT_STENCIL5>;
   else if (m.dense) k = soft ? bellman_numpy_order_kernel<true, IRLMX_LAYOUT_DENSE>
                              : bellman_numpy_order_kernel<false, IRLMX_LAYOUT_DENSE>;
@@ -2666,8 +2779,9 @@ static int bellman_numpy_order(const irlmx_mdp* mdp, const double* reward, const
   const size_t lds = 2 * (size_t)m.S * sizeof(double) + 4 * sizeof(unsigned long long);
   hipError_t e = hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
   if (e != hipSuccess) return hip_fail(e, "hipFuncSetAttribute");
-  hipLaunchKernelGGL(k, dim3(m.B), dim3(m.S >= 1024 ? 1024 : ((m.S + kWave - 1) / kWave) * kWave), lds,
-                     (hipStream_t)stream, a);
+  const int nthr = cached ? std::min(kNpCachedThreads, ((m.S + kWave - 1) / kWave) * kWave)
+                          : (m.S >= 1024 ? 1024 : ((m.S + kWave - 1) / kWave) * kWave);
+  hipLaunchKernelGGL(k, dim3(m.B), dim3(nthr), lds, (hipStream_t)stream, a);
   e = hipGetLastError();
   return e == hipSuccess ? 0 : hip_fail(e, fn);
 }
