@@ -803,33 +803,34 @@ __global__ void __launch_bounds__(kNpCachedThreads) fwd_numpy_order_cached_kerne
       double dv[kStencilK];
 #pragma unroll
       for (int i = 0; i < kStencilK; ++i) dv[i] = i < n[j] ? d[src[j][i]] : 0.0;
+      // all actions' chains side by side, branch-free (the entries' kinds differ
+      // between lanes): every step computes its candidates and selects, so the
+      // four independent chains interleave instead of diverging
+      double out[kNpCachedMaxActions], c[kNpCachedMaxActions];
+#pragma unroll
+      for (int act = 0; act < kNpCachedMaxActions; ++act) { out[act] = 0.0; c[act] = 0.0; }
+      bool open = false;
+#pragma unroll
+      for (int i = 0; i < kStencilK; ++i) {
+        const int kd = i < n[j] ? kind[j][i] : -1;  // -1: no entry
+        const bool flush = open && (kd == 1 || kd == 2);
+#pragma unroll
+        for (int act = 0; act < kNpCachedMaxActions; ++act) {
+          const double vv = val[j][act][i];
+          const double x = __dmul_rn(pw[j][act][i], dv[i]);  // maxent.py:109
+          const double o1 = flush ? __dadd_rn(out[act], c[act]) : out[act];
+          const double cf = fma(vv, x, kd == 1 ? 0.0 : c[act]);
+          c[act] = (kd == 0 || kd == 1) ? cf : c[act];
+          out[act] = kd == 3 ? fma(vv, x, out[act]) : (kd == 2 ? __dadd_rn(o1, __dmul_rn(vv, x)) : o1);
+        }
+        open = kd == 1 ? true : (kd == 2 ? false : open);
+      }
       double v = 0.0;
 #pragma unroll
       for (int act = 0; act < kNpCachedMaxActions; ++act) {
         if (act >= A) break;
-        double out = 0.0, c = 0.0;
-        bool open = false;
-#pragma unroll
-        for (int i = 0; i < kStencilK; ++i) {
-          if (i >= n[j]) break;
-          const double x = __dmul_rn(pw[j][act][i], dv[i]);  // maxent.py:109
-          const int kd = kind[j][i];
-          if (kd == 3) {
-            out = fma(val[j][act][i], x, out);
-          } else if (kd == 2) {
-            if (open) { out = __dadd_rn(out, c); open = false; }
-            out = __dadd_rn(out, __dmul_rn(val[j][act][i], x));
-          } else {
-            if (kd == 1) {
-              if (open) out = __dadd_rn(out, c);
-              c = 0.0;
-              open = true;
-            }
-            c = fma(val[j][act][i], x, c);
-          }
-        }
-        if (open) out = __dadd_rn(out, c);
-        const double y = poisoned ? kNaN : out;
+        const double o = open ? __dadd_rn(out[act], c[act]) : out[act];
+        const double y = poisoned ? kNaN : o;
         v = act == 0 ? y : __dadd_rn(v, y);  // np.array(d_).sum(axis=0)
       }
       const double nv = __dadd_rn(p0t[j], v);  // maxent.py:110
