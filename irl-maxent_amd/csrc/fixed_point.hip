@@ -643,15 +643,16 @@ __global__ void __launch_bounds__(1024) fwd_numpy_order_kernel(NpFwdArgs a) {
   const Model& m = a.m;
   const int S = m.S, A = m.A;
   const int b = blockIdx.x, tid = threadIdx.x, nt = blockDim.x;
-  double* buf[2] = {(double*)smem, (double*)smem + S};
-  unsigned long long* slot = (unsigned long long*)(buf[1] + S);  // [3] delta ring
+  double* const buf0 = (double*)smem;  // (two named LDS pointers, not an array: ds_* accesses, not flat)
+  double* const buf1 = buf0 + S;
+  unsigned long long* slot = (unsigned long long*)(buf1 + S);  // [3] delta ring
   int* bad = (int*)(slot + 3);                                     // [2] sticky non-finite, by parity
   const double* pi = a.pi + (size_t)b * S * A;
   const double* p0 = a.p0 + (size_t)b * S;
   const uint8_t* term = a.term + (size_t)b * S;
   bool nf = false;
   for (int s = tid; s < S; s += nt) {
-    buf[0][s] = 0.0;  // maxent.py:105
+    buf0[s] = 0.0;  // maxent.py:105
     for (int act = 0; act < A; ++act) nf |= !isfinite(pi[(size_t)s * A + act]);
   }
   if (tid < 3) slot[tid] = 0ull;
@@ -663,8 +664,8 @@ __global__ void __launch_bounds__(1024) fwd_numpy_order_kernel(NpFwdArgs a) {
   int r3 = 0;
   double delta = 0.0;
   for (;;) {
-    const double* d = buf[it & 1];
-    double* dn = buf[(it & 1) ^ 1];
+    const double* d = ((it & 1) ? buf1 : buf0);
+    double* dn = ((it & 1) ? buf0 : buf1);
     const bool poisoned = bad[(it & 1) ^ 1] != 0;  // written in the previous sweep (or above)
     unsigned long long mx = 0ull;
     bool nfo = false;
@@ -692,7 +693,7 @@ __global__ void __launch_bounds__(1024) fwd_numpy_order_kernel(NpFwdArgs a) {
     if (!(delta > a.eps)) break;  // maxent.py:108
     if (a.max_iter > 0 && it >= a.max_iter) break;
   }
-  const double* d = buf[it & 1];
+  const double* d = ((it & 1) ? buf1 : buf0);
   for (int t = tid; t < S; t += nt) a.svf[(size_t)b * S + t] = d[t];
   if (tid == 0) {
     a.iters[b] = it;
@@ -715,8 +716,9 @@ __global__ void __launch_bounds__(kNpCachedThreads) fwd_numpy_order_cached_kerne
   const Model& m = a.m;
   const int S = m.S, A = m.A, n4 = S & ~3;
   const int b = blockIdx.x, tid = threadIdx.x, nt = blockDim.x;
-  double* buf[2] = {(double*)smem, (double*)smem + S};
-  unsigned long long* slot = (unsigned long long*)(buf[1] + S);
+  double* const buf0 = (double*)smem;  // (two named LDS pointers, not an array: ds_* accesses, not flat)
+  double* const buf1 = buf0 + S;
+  unsigned long long* slot = (unsigned long long*)(buf1 + S);
   int* bad = (int*)(slot + 3);
   const double* pi = a.pi + (size_t)b * S * A;
   const uint8_t* term = a.term + (size_t)b * S;
@@ -779,7 +781,7 @@ __global__ void __launch_bounds__(kNpCachedThreads) fwd_numpy_order_cached_kerne
   }
   bool nf = false;
   for (int s = tid; s < S; s += nt) {
-    buf[0][s] = 0.0;  // maxent.py:105
+    buf0[s] = 0.0;  // maxent.py:105
     for (int act = 0; act < A; ++act) nf |= !isfinite(pi[(size_t)s * A + act]);
   }
   if (tid < 3) slot[tid] = 0ull;
@@ -791,8 +793,8 @@ __global__ void __launch_bounds__(kNpCachedThreads) fwd_numpy_order_cached_kerne
   int r3 = 0;
   double delta = 0.0;
   for (;;) {
-    const double* d = buf[it & 1];
-    double* dn = buf[(it & 1) ^ 1];
+    const double* d = ((it & 1) ? buf1 : buf0);
+    double* dn = ((it & 1) ? buf0 : buf1);
     const bool poisoned = bad[(it & 1) ^ 1] != 0;
     unsigned long long mx = 0ull;
     bool nfo = false;
@@ -850,7 +852,7 @@ __global__ void __launch_bounds__(kNpCachedThreads) fwd_numpy_order_cached_kerne
     if (!(delta > a.eps)) break;  // maxent.py:108
     if (a.max_iter > 0 && it >= a.max_iter) break;
   }
-  for (int t = tid; t < S; t += nt) a.svf[(size_t)b * S + t] = buf[it & 1][t];
+  for (int t = tid; t < S; t += nt) a.svf[(size_t)b * S + t] = ((it & 1) ? buf1 : buf0)[t];
   if (tid == 0) {
     a.iters[b] = it;
     a.status[b] = finish_status(delta, a.eps);
@@ -915,8 +917,9 @@ __global__ void __launch_bounds__(kNpCachedThreads) bwd_numpy_order_cached_kerne
   const Model& m = a.m;
   const int S = m.S, A = m.A, m1 = S & ~3;
   const int b = blockIdx.x, tid = threadIdx.x, nt = blockDim.x;
-  double* zbuf[2] = {(double*)smem, (double*)smem + S};
-  int* bad = (int*)(zbuf[1] + S);
+  double* const zbuf0 = (double*)smem;  // (two named LDS pointers, not an array: ds_* accesses, not flat)
+  double* const zbuf1 = zbuf0 + S;
+  int* bad = (int*)(zbuf1 + S);
   const double* er = a.er + (size_t)b * S;
   double* pi = a.pi + (size_t)b * S * A;
   NpStencilRows<TPT> rows;
@@ -924,13 +927,13 @@ __global__ void __launch_bounds__(kNpCachedThreads) bwd_numpy_order_cached_kerne
   double ers[TPT];
 #pragma unroll
   for (int j = 0; j < TPT; ++j) ers[j] = tid + j * nt < S ? er[tid + j * nt] : 0.0;
-  for (int s = tid; s < S; s += nt) zbuf[0][s] = a.term[(size_t)b * S + s] ? 1.0 : 0.0;  // maxent.py:146-147
+  for (int s = tid; s < S; s += nt) zbuf0[s] = a.term[(size_t)b * S + s] ? 1.0 : 0.0;  // maxent.py:146-147
   if (tid < 2) bad[tid] = 0;
   __syncthreads();
   const long long n = 2LL * S;  // maxent.py:154
   for (long long it = 0; it < n; ++it) {
-    const double* zin = zbuf[it & 1];
-    double* zout = zbuf[(it & 1) ^ 1];
+    const double* zin = ((it & 1) ? zbuf1 : zbuf0);
+    double* zout = ((it & 1) ? zbuf0 : zbuf1);
     if (it > 0 && bad[(it - 1) & 1]) {  // the reference's overflow: NaN from here on (bwd_numpy_order_kernel)
       for (int s = tid; s < S; s += nt)
         for (int act = 0; act < A; ++act) pi[(size_t)s * A + act] = kNaN;
@@ -958,7 +961,7 @@ __global__ void __launch_bounds__(kNpCachedThreads) bwd_numpy_order_cached_kerne
     if (nf) bad[it & 1] = 1;
     __syncthreads();
   }
-  const double* zs = zbuf[n & 1];
+  const double* zs = ((n & 1) ? zbuf1 : zbuf0);
   for (int s = tid; s < S; s += nt)
     for (int act = 0; act < A; ++act) pi[(size_t)s * A + act] = pi[(size_t)s * A + act] / zs[s];  // maxent.py:159
   if (tid == 0) a.status[b] = IRLMX_OK;
@@ -970,17 +973,18 @@ __global__ void __launch_bounds__(1024) bwd_numpy_order_kernel(NpArgs a) {
   const Model& m = a.m;
   const int S = m.S, A = m.A;
   const int b = blockIdx.x, tid = threadIdx.x, nt = blockDim.x;
-  double* zbuf[2] = {(double*)smem, (double*)smem + S};
-  int* bad = (int*)(zbuf[1] + S);  // [2] sticky: sweep k's output had a non-finite value (slot k & 1)
+  double* const zbuf0 = (double*)smem;  // (two named LDS pointers, not an array: ds_* accesses, not flat)
+  double* const zbuf1 = zbuf0 + S;
+  int* bad = (int*)(zbuf1 + S);  // [2] sticky: sweep k's output had a non-finite value (slot k & 1)
   const double* er = a.er + (size_t)b * S;
   double* pi = a.pi + (size_t)b * S * A;
-  for (int s = tid; s < S; s += nt) zbuf[0][s] = a.term[(size_t)b * S + s] ? 1.0 : 0.0;  // maxent.py:146-147
+  for (int s = tid; s < S; s += nt) zbuf0[s] = a.term[(size_t)b * S + s] ? 1.0 : 0.0;  // maxent.py:146-147
   if (tid < 2) bad[tid] = 0;
   __syncthreads();
   const long long n = 2LL * S;  // maxent.py:154
   for (long long it = 0; it < n; ++it) {
-    const double* zin = zbuf[it & 1];
-    double* zout = zbuf[(it & 1) ^ 1];
+    const double* zin = ((it & 1) ? zbuf1 : zbuf0);
+    double* zout = ((it & 1) ? zbuf0 : zbuf1);
     // a non-finite zs meets a zero entry of every dense row (0 * inf): the
     // reference's next dots are all NaN (a DENSE row visits every column itself)
     const bool poisoned = LAYOUT != IRLMX_LAYOUT_DENSE && it > 0 && bad[(it - 1) & 1];
@@ -1007,7 +1011,7 @@ __global__ void __launch_bounds__(1024) bwd_numpy_order_kernel(NpArgs a) {
     if (nf) bad[it & 1] = 1;
     __syncthreads();
   }
-  const double* zs = zbuf[n & 1];
+  const double* zs = ((n & 1) ? zbuf1 : zbuf0);
   for (int s = tid; s < S; s += nt)
     for (int act = 0; act < A; ++act) pi[(size_t)s * A + act] = pi[(size_t)s * A + act] / zs[s];  // maxent.py:159
   if (tid == 0) a.status[b] = IRLMX_OK;
@@ -1163,19 +1167,20 @@ __global__ void __launch_bounds__(1024) bellman_numpy_order_kernel(SoftArgs a) {
   const Model& m = a.m;
   const int S = m.S, A = m.A;
   const int b = blockIdx.x, tid = threadIdx.x, nt = blockDim.x;
-  double* buf[2] = {(double*)smem, (double*)smem + S};
-  unsigned long long* slot = (unsigned long long*)(buf[1] + S);
+  double* const buf0 = (double*)smem;  // (two named LDS pointers, not an array: ds_* accesses, not flat)
+  double* const buf1 = buf0 + S;
+  unsigned long long* slot = (unsigned long long*)(buf1 + S);
   const double v0 = SOFT ? -1e200 : 0.0;  // maxent.py:323 / solver.py:29
   const double* rw = a.reward + (size_t)b * S;
-  for (int s = tid; s < S; s += nt) buf[0][s] = v0;
+  for (int s = tid; s < S; s += nt) buf0[s] = v0;
   if (tid < 3) slot[tid] = 0ull;
   __syncthreads();
   long long it = 0;
   int r3 = 0;
   double delta = 0.0;
   for (;;) {
-    const double* vin = buf[it & 1];
-    double* vout = buf[(it & 1) ^ 1];
+    const double* vin = ((it & 1) ? buf1 : buf0);
+    double* vout = ((it & 1) ? buf0 : buf1);
     unsigned long long mx = 0ull;
     for (int s = tid; s < S; s += nt) {
       const double r = rw[s];
@@ -1205,8 +1210,8 @@ __global__ void __launch_bounds__(1024) bellman_numpy_order_kernel(SoftArgs a) {
     if (!(delta > a.eps)) break;
     if (a.max_iter > 0 && it >= a.max_iter) break;
   }
-  const double* vold = buf[(it & 1) ^ 1];  // input of the last sweep
-  const double* vnew = buf[it & 1];
+  const double* vold = ((it & 1) ? buf0 : buf1);  // input of the last sweep
+  const double* vnew = ((it & 1) ? buf1 : buf0);
   for (int s = tid; s < S; s += nt) {
     if (a.value) a.value[(size_t)b * S + s] = vnew[s];
     if (SOFT)
@@ -1229,8 +1234,9 @@ __global__ void __launch_bounds__(kNpCachedThreads) bellman_numpy_order_cached_k
   const Model& m = a.m;
   const int S = m.S, A = m.A, m1 = S & ~3;
   const int b = blockIdx.x, tid = threadIdx.x, nt = blockDim.x;
-  double* buf[2] = {(double*)smem, (double*)smem + S};
-  unsigned long long* slot = (unsigned long long*)(buf[1] + S);
+  double* const buf0 = (double*)smem;  // (two named LDS pointers, not an array: ds_* accesses, not flat)
+  double* const buf1 = buf0 + S;
+  unsigned long long* slot = (unsigned long long*)(buf1 + S);
   const double v0 = SOFT ? -1e200 : 0.0;  // maxent.py:323 / solver.py:29
   NpStencilRows<TPT> rows;
   rows.load(m, b, tid, nt);
@@ -1241,15 +1247,15 @@ __global__ void __launch_bounds__(kNpCachedThreads) bellman_numpy_order_cached_k
     rr[j] = s < S ? a.reward[(size_t)b * S + s] : 0.0;
     ph[j] = (SOFT && s < S) ? a.phi[(size_t)b * S + s] : 0.0;
   }
-  for (int s = tid; s < S; s += nt) buf[0][s] = v0;
+  for (int s = tid; s < S; s += nt) buf0[s] = v0;
   if (tid < 3) slot[tid] = 0ull;
   __syncthreads();
   long long it = 0;
   int r3 = 0;
   double delta = 0.0;
   for (;;) {
-    const double* vin = buf[it & 1];
-    double* vout = buf[(it & 1) ^ 1];
+    const double* vin = ((it & 1) ? buf1 : buf0);
+    double* vout = ((it & 1) ? buf0 : buf1);
     unsigned long long mx = 0ull;
 #pragma unroll
     for (int j = 0; j < TPT; ++j) {
@@ -1285,8 +1291,8 @@ __global__ void __launch_bounds__(kNpCachedThreads) bellman_numpy_order_cached_k
     if (!(delta > a.eps)) break;
     if (a.max_iter > 0 && it >= a.max_iter) break;
   }
-  const double* vold = buf[(it & 1) ^ 1];  // input of the last sweep
-  const double* vnew = buf[it & 1];
+  const double* vold = ((it & 1) ? buf0 : buf1);  // input of the last sweep
+  const double* vnew = ((it & 1) ? buf1 : buf0);
 #pragma unroll
   for (int j = 0; j < TPT; ++j) {
     const int s = tid + j * nt;
