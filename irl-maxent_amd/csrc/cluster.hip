@@ -110,6 +110,11 @@ __global__ void __launch_bounds__(NT) cluster_kernel(ClusterArgs a) {
   // COLS pairs: band edge rows' side neighbours from LDS (for quads, where 2 of
   // 3 rows are edge rows, the exposed LDS latency costs more than the DPP moves)
   constexpr bool kLdsSides = COLS && CPL == 2 && IRLMX_LDS_SIDES;
+#ifndef IRLMX_COLS_RELOAD
+#define IRLMX_COLS_RELOAD 0
+#endif
+  // COLS: register state through the LDS tile at every block boundary (see the publish step)
+  constexpr bool kReload = COLS && IRLMX_COLS_RELOAD;
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   const int W = WT ? WT : a.W;
   const int H = a.H, S = a.S;
@@ -517,9 +522,15 @@ __global__ void __launch_bounds__(NT) cluster_kernel(ClusterArgs a) {
   double* oth = bufB;
   long long done = 0;  // sweeps completed before the current block
   // phase cycle counters (thread 0): sweeps, summary + publish, exchange wait, refresh, blocks
-  unsigned long long st_acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};  // [5], [6]: sub-phases of 1
+  // (in LDS, thread 0 only: as registers they are live across the sweep loop and
+  // push the quad kernels over their register budget)
+  __shared__ unsigned long long st_acc[8], ts_l[1];  // st_acc[5], [6]: sub-phases of 1
   const bool stamps = a.stamps != nullptr && tid == 0;
-  unsigned long long ts = stamps ? stamp_now() : 0;
+  if (stamps) {
+    for (int k = 0; k < 8; ++k) st_acc[k] = 0ull;
+    ts_l[0] = stamp_now();
+  }
+  unsigned long long& ts = ts_l[0];
   auto stamp = [&](int k) {
     if (stamps) { const unsigned long long t = stamp_now(); st_acc[k] += t - ts; ts = t; }
   };
@@ -618,8 +629,11 @@ __global__ void __launch_bounds__(NT) cluster_kernel(ClusterArgs a) {
     };
     if constexpr (COLS) {
       // a band's rows sit in one wave: stage them in the LDS tile first, so that
-      // the stores spread over all waves after the barrier below
-      const unsigned pb = slot_bits(pub_bits);
+      // the stores spread over all waves after the barrier below.  kReload: all
+      // owned rows, and the register state is read back from the tile after the
+      // exchange -- it is then not live across the exchange code, which fits the
+      // kernels in their register budget without scratch spills.
+      const unsigned pb = slot_bits(kReload ? own_bits : pub_bits);
 #pragma unroll
       for (int jp = 0; jp < SPT / 2; ++jp)
         if ((pb >> (2 * jp)) & 1u)
@@ -765,7 +779,8 @@ __global__ void __launch_bounds__(NT) cluster_kernel(ClusterArgs a) {
         const int l = slot_state(2 * jp);
         const bool own = (ob >> (2 * jp)) & 1u, ext = (xb >> (2 * jp)) & 1u;
         double2 v = make_double2(cv[PAIR ? 2 * jp : 0], cv[PAIR ? 2 * jp + 1 : 0]);
-        if (!own && ext) v = *reinterpret_cast<const double2*>(cur + pad + l);  // gathered ghost pair
+        if (kReload) v = ext ? *reinterpret_cast<const double2*>(cur + pad + l) : make_double2(0.0, 0.0);
+        else if (!own && ext) v = *reinterpret_cast<const double2*>(cur + pad + l);  // gathered ghost pair
         if (MODE == kModeBwd && e_scale) {
           v.x = ldexp(v.x, e_scale);
           v.y = ldexp(v.y, e_scale);
@@ -929,7 +944,7 @@ bool cluster_plan(int W, int H, int B, int mode, ClusterPlan* out) {
       if (pair) spt = (spt + (layout == 3 ? 3 : 1)) / (layout == 3 ? 4 : 2) * (layout == 3 ? 4 : 2);
       if (spt > spt_max) continue;
       const size_t lds = cluster_lds(spt * nt, W, layout, nt, mode);
-      if (lds > kMaxLdsBytes) continue;
+      if (lds + kClusterStaticLds > kMaxLdsBytes) continue;
       const int per = cus / C;
       if (per < 1) continue;
       const int nl = (B + per - 1) / per;
@@ -1001,7 +1016,9 @@ static void* cluster_fn_quad(int spt) {
     case 4: return (void*)&cluster_kernel<MODE, 4, WT, 3, kPairThreads>;
     case 8: return (void*)&cluster_kernel<MODE, 8, WT, 3, kPairThreads>;
     case 12: return (void*)&cluster_kernel<MODE, 12, WT, 3, kPairThreads>;
-    case 16: return (void*)&cluster_kernel<MODE, 16, WT, 3, kPairThreads>;
+    case 16:  // backward only (kSptMaxQuadFwd: the forward does not fit its registers)
+      if constexpr (MODE == kModeBwd) return (void*)&cluster_kernel<MODE, 16, WT, 3, kPairThreads>;
+      return nullptr;
   }
   return nullptr;
 }
