@@ -393,8 +393,15 @@ __global__ void __launch_bounds__(NT) cluster_kernel(ClusterArgs a) {
       // reads an adjacent, finite array entry.
       double side[2][2];  // [top, bottom][left, right]
       // (which: 1 = the row above, 2 = the row below, 3 = both; sync: the barrier first)
+#ifndef IRLMX_PIN_BARRIER
+#define IRLMX_PIN_BARRIER 0
+#endif
       auto edges_in = [&](int which = 3, bool sync = true) {
+        // (IRLMX_PIN_BARRIER: keep the instruction scheduler from moving the
+        // interior rows' FMAs across the barrier)
+        if (IRLMX_PIN_BARRIER && sync) __builtin_amdgcn_sched_barrier(0);
         if (sync) __syncthreads();
+        if (IRLMX_PIN_BARRIER && sync) __builtin_amdgcn_sched_barrier(0);
         const double2* t = bnd_at(i & 1, bb, 1);
         const double2* u = bnd_at(i & 1, bb + 2, 0);
 #pragma unroll
