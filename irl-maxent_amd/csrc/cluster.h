@@ -19,7 +19,10 @@ constexpr int kSptMaxQuadFwd = 12;  // forward with column quads (register budge
 constexpr int kSptMaxQuadBwd = 16;
 constexpr int kTMax = 16;          // max sweeps per block (= max ghost rows)
 constexpr int kSoloBwdT = 256;     // backward sweeps per block of a solo tile (no ghost rows)
-constexpr int kRescaleEvery = 4;   // backward: max blocks between rescales
+#ifndef IRLMX_RESCALE_EVERY
+#define IRLMX_RESCALE_EVERY 4
+#endif
+constexpr int kRescaleEvery = IRLMX_RESCALE_EVERY;  // backward: max blocks between rescales
 constexpr size_t kMaxLdsBytes = 160 * 1024;  // LDS per CU (one workgroup per CU)
 constexpr size_t kClusterStaticLds = 128;     // cluster_kernel's own __shared__ variables (resident flag, stamps)
 constexpr int kModeFwd = 0;

@@ -701,6 +701,14 @@ __global__ void __launch_bounds__(NT) cluster_kernel(ClusterArgs a) {
     // ---- all polls of a thread in flight together: one round trip --------------
     bool ok = true;
     constexpr int GPT = PAIR ? kGatherPerThread : 1;  // ghost granules in flight per thread
+    // Every tile's summary is waited for only when the block needs it (the
+    // forward's convergence bits, the backward's rescale blocks): between
+    // rescales a backward tile waits for its two neighbours' rows alone, not
+    // for the slowest of the instance's C tiles.
+#ifndef IRLMX_LAZY_SUMMARY
+#define IRLMX_LAZY_SUMMARY 1
+#endif
+    const bool need_summary = !IRLMX_LAZY_SUMMARY || MODE == kModeFwd || resc;
     auto gather = [&]() {
       for (int k0 = 0; k0 < max(ng, 1); k0 += GPT * NT) {
         unsigned off[GPT + 1];
@@ -714,7 +722,7 @@ __global__ void __launch_bounds__(NT) cluster_kernel(ClusterArgs a) {
           want |= (k < ng ? 1u : 0u) << i;
         }
         off[GPT] = ((unsigned)(m & 1) * (unsigned)a.H + (unsigned)tid) * 16u;
-        want |= (k0 == 0 && tid < a.C ? 1u : 0u) << GPT;
+        want |= (k0 == 0 && tid < a.C && need_summary ? 1u : 0u) << GPT;
         unsigned long long v[GPT + 1];
         ok &= gran_gather<GPT + 1>(rg, rs, off, want, tag, v, a.gather_ticks);
 #pragma unroll

@@ -789,14 +789,22 @@ __global__ void __launch_bounds__(kNpCachedThreads) fwd_numpy_order_cached_kerne
   __syncthreads();
   if (nf) bad[1] = 1;
   __syncthreads();
+  // Convergence deferred over blocks of kNpFwdBlock sweeps: each lane records
+  // per sweep i "some |d_ - d| > eps" (bit i) and "some |d_ - d| is NaN" (bit
+  // 32 + i) for its targets, and the workgroup ORs the bits once per block --
+  // no per-sweep max reduction (its six cross-lane steps were most of a
+  // sweep's latency).  The reference stops after the first sweep whose
+  // np.max|d_ - d| is not > eps, NaN included (maxent.py:108): if a block holds
+  // that sweep, the block-start state (kept in registers) goes back into LDS and
+  // the sweeps up to it are replayed -- the same arithmetic, so the same bits.
+  constexpr int kNpFwdBlock = 32;
   long long it = 0;
-  int r3 = 0;
-  double delta = 0.0;
-  for (;;) {
+  int status = IRLMX_OK;
+  // one sweep from buffer parity it & 1, its bits recorded at position pos
+  auto sweep = [&](long long it, int pos, unsigned long long& bits) __attribute__((always_inline)) {
     const double* d = ((it & 1) ? buf1 : buf0);
     double* dn = ((it & 1) ? buf0 : buf1);
     const bool poisoned = bad[(it & 1) ^ 1] != 0;
-    unsigned long long mx = 0ull;
     bool nfo = false;
 #pragma unroll
     for (int j = 0; j < TPT; ++j) {
@@ -838,24 +846,63 @@ __global__ void __launch_bounds__(kNpCachedThreads) fwd_numpy_order_cached_kerne
       const double nv = __dadd_rn(p0t[j], v);  // maxent.py:110
       dn[t] = nv;
       nfo |= !isfinite(nv);
-      const unsigned long long dd = abs_bits(nv - d[t]);
-      mx = dd > mx ? dd : mx;
+      const double dd = fabs(nv - d[t]);
+      bits |= ((dd > a.eps) ? 1ull : 0ull) << pos;
+      bits |= ((dd != dd) ? 1ull : 0ull) << (32 + pos);
     }
     if (nfo) bad[it & 1] = 1;
-    mx = wave_max_u64(mx);
-    if ((tid & (kWave - 1)) == 0 && mx) atomicMax(&slot[r3], mx);
-    if (tid == 0) slot[r3 == 2 ? 0 : r3 + 1] = 0ull;
     __syncthreads();
-    delta = bits_double(slot[r3]);
-    r3 = r3 == 2 ? 0 : r3 + 1;
-    ++it;
-    if (!(delta > a.eps)) break;  // maxent.py:108
-    if (a.max_iter > 0 && it >= a.max_iter) break;
+  };
+  for (int blk = 0;; ++blk) {
+    double keep[TPT];
+    const double* d0 = ((it & 1) ? buf1 : buf0);
+#pragma unroll
+    for (int j = 0; j < TPT; ++j) keep[j] = tid + j * nt < S ? d0[tid + j * nt] : 0.0;
+    const int bad0 = bad[0], bad1 = bad[1];
+    int nb = kNpFwdBlock;
+    if (a.max_iter > 0) nb = (int)min<long long>(nb, a.max_iter - it);
+    // pass 0: the block with its bits; pass 1 (the stop inside the block): the
+    // replay from the block start up to the stopping sweep k (one call site of
+    // the sweep, so it is inlined once)
+    int k = -1;
+    unsigned nan = 0u;
+    for (int pass = 0; pass < 2; ++pass) {
+      unsigned long long bits = 0ull;
+      const int cnt = pass == 0 ? nb : k + 1;
+      for (int i = 0; i < cnt; ++i) sweep(it + i, i, bits);
+      if (pass == 1) break;
+      bits = wave_or_u64(bits);
+      if ((tid & (kWave - 1)) == 0 && bits) atomicOr(&slot[blk & 1], bits);
+      if (tid == 0) slot[(blk & 1) ^ 1] = 0ull;  // last read in the previous block, before this block's barriers
+      __syncthreads();
+      const unsigned long long all = slot[blk & 1];
+      const unsigned gt = (unsigned)all;
+      nan = (unsigned)(all >> 32);
+      const unsigned live = nb >= 32 ? 0xFFFFFFFFu : ((1u << nb) - 1u);
+      const unsigned stop = (~gt | nan) & live;
+      if (!stop) break;
+      // the stopping sweep is inside this block: back to its start
+      k = __builtin_ctz(stop);
+      double* d0w = ((it & 1) ? buf1 : buf0);
+#pragma unroll
+      for (int j = 0; j < TPT; ++j)
+        if (tid + j * nt < S) d0w[tid + j * nt] = keep[j];
+      __syncthreads();  // every lane past its reads of bad[] before they are restored
+      if (tid == 0) { bad[0] = bad0; bad[1] = bad1; }
+      __syncthreads();
+    }
+    if (k >= 0) {
+      it += k + 1;
+      status = ((nan >> k) & 1u) ? IRLMX_NONFINITE : IRLMX_OK;
+      break;
+    }
+    it += nb;
+    if (a.max_iter > 0 && it >= a.max_iter) { status = IRLMX_MAXITER; break; }
   }
   for (int t = tid; t < S; t += nt) a.svf[(size_t)b * S + t] = ((it & 1) ? buf1 : buf0)[t];
   if (tid == 0) {
     a.iters[b] = it;
-    a.status[b] = finish_status(delta, a.eps);
+    a.status[b] = status;
   }
 }
 
@@ -870,7 +917,7 @@ struct NpStencilRows {
   int col[TPT][kStencilK], lane[TPT][kStencilK];
   double val[TPT][kNpCachedMaxActions][kStencilK];
 
-  __device__ void load(const Model& m, int b, int tid, int nt) {
+  __device__ __attribute__((always_inline)) void load(const Model& m, int b, int tid, int nt) {
     constexpr int order[kStencilK] = {4, 2, 0, 1, 3};
     const int S = m.S, m1 = S & ~3;
 #pragma unroll
@@ -888,12 +935,12 @@ struct NpStencilRows {
     }
   }
   // the vector at state j's columns
-  __device__ void gather(int j, const double* v, double (&x)[kStencilK]) const {
+  __device__ __attribute__((always_inline)) void gather(int j, const double* v, double (&x)[kStencilK]) const {
 #pragma unroll
     for (int i = 0; i < kStencilK; ++i) x[i] = lane[j][i] >= 0 ? v[col[j][i]] : 0.0;
   }
   // p[act][s, :] . v in OpenBLAS dgemv_t order (fused: rows s < S & ~3)
-  __device__ double dot(int j, int act, bool fused, const double (&x)[kStencilK]) const {
+  __device__ __attribute__((always_inline)) double dot(int j, int act, bool fused, const double (&x)[kStencilK]) const {
     double l[4] = {0.0, 0.0, 0.0, 0.0};
 #pragma unroll
     for (int q = 0; q < 4; ++q)
@@ -1250,13 +1297,15 @@ __global__ void __launch_bounds__(kNpCachedThreads) bellman_numpy_order_cached_k
   for (int s = tid; s < S; s += nt) buf0[s] = v0;
   if (tid < 3) slot[tid] = 0ull;
   __syncthreads();
+  // convergence deferred over blocks of 32 sweeps, replay of the stopping
+  // block: as in fwd_numpy_order_cached_kernel (the stop after the first sweep
+  // whose max|v_new - v| is not > eps, NaN included: solver.py:49, maxent.py:335)
+  constexpr int kNpBlock = 32;
   long long it = 0;
-  int r3 = 0;
-  double delta = 0.0;
-  for (;;) {
+  int status = IRLMX_OK;
+  auto sweep = [&](long long it, int pos, unsigned long long& bits) __attribute__((always_inline)) {
     const double* vin = ((it & 1) ? buf1 : buf0);
     double* vout = ((it & 1) ? buf0 : buf1);
-    unsigned long long mx = 0ull;
 #pragma unroll
     for (int j = 0; j < TPT; ++j) {
       const int s = tid + j * nt;
@@ -1278,18 +1327,50 @@ __global__ void __launch_bounds__(kNpCachedThreads) bellman_numpy_order_cached_k
       }
       if (!SOFT) v = __dadd_rn(rr[j], a.average ? v / (double)A : v);  // solver.py:47 / :99
       vout[s] = v;
-      const unsigned long long d = abs_bits(v - vin[s]);
-      mx = d > mx ? d : mx;
+      const double d = fabs(v - vin[s]);
+      bits |= ((d > a.eps) ? 1ull : 0ull) << pos;
+      bits |= ((d != d) ? 1ull : 0ull) << (32 + pos);
     }
-    mx = wave_max_u64(mx);
-    if ((tid & (kWave - 1)) == 0 && mx) atomicMax(&slot[r3], mx);
-    if (tid == 0) slot[r3 == 2 ? 0 : r3 + 1] = 0ull;
     __syncthreads();
-    delta = bits_double(slot[r3]);
-    r3 = r3 == 2 ? 0 : r3 + 1;
-    ++it;
-    if (!(delta > a.eps)) break;
-    if (a.max_iter > 0 && it >= a.max_iter) break;
+  };
+  for (int blk = 0;; ++blk) {
+    double keep[TPT];
+    const double* v0p = ((it & 1) ? buf1 : buf0);
+#pragma unroll
+    for (int j = 0; j < TPT; ++j) keep[j] = tid + j * nt < S ? v0p[tid + j * nt] : 0.0;
+    int nb = kNpBlock;
+    if (a.max_iter > 0) nb = (int)min<long long>(nb, a.max_iter - it);
+    int k = -1;
+    unsigned nan = 0u;
+    for (int pass = 0; pass < 2; ++pass) {  // the block, then (stop inside it) the replay
+      unsigned long long bits = 0ull;
+      const int cnt = pass == 0 ? nb : k + 1;
+      for (int i = 0; i < cnt; ++i) sweep(it + i, i, bits);
+      if (pass == 1) break;
+      bits = wave_or_u64(bits);
+      if ((tid & (kWave - 1)) == 0 && bits) atomicOr(&slot[blk & 1], bits);
+      if (tid == 0) slot[(blk & 1) ^ 1] = 0ull;  // last read in the previous block, before this block's barriers
+      __syncthreads();
+      const unsigned long long all = slot[blk & 1];
+      const unsigned gt = (unsigned)all;
+      nan = (unsigned)(all >> 32);
+      const unsigned live = nb >= 32 ? 0xFFFFFFFFu : ((1u << nb) - 1u);
+      const unsigned stop = (~gt | nan) & live;
+      if (!stop) break;
+      k = __builtin_ctz(stop);
+      double* v0w = ((it & 1) ? buf1 : buf0);
+#pragma unroll
+      for (int j = 0; j < TPT; ++j)
+        if (tid + j * nt < S) v0w[tid + j * nt] = keep[j];
+      __syncthreads();
+    }
+    if (k >= 0) {
+      it += k + 1;
+      status = ((nan >> k) & 1u) ? IRLMX_NONFINITE : IRLMX_OK;
+      break;
+    }
+    it += nb;
+    if (a.max_iter > 0 && it >= a.max_iter) { status = IRLMX_MAXITER; break; }
   }
   const double* vold = ((it & 1) ? buf0 : buf1);  // input of the last sweep
   const double* vnew = ((it & 1) ? buf1 : buf0);
@@ -1311,7 +1392,7 @@ __global__ void __launch_bounds__(kNpCachedThreads) bellman_numpy_order_cached_k
   }
   if (tid == 0) {
     if (a.iters) a.iters[b] = it;
-    a.status[b] = finish_status(delta, a.eps);
+    a.status[b] = status;
   }
 }
 

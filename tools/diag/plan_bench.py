@@ -41,8 +41,9 @@ for v in sys.argv[1:] or [""]:
     if ref is None:
         ref = out
     sweeps = int(out[1].max()) if mode == "fwd" else 2 * n
+    pl = ops.execution_plan(mdp, "forward" if mode == "fwd" else "backward")
     print(f"[{v or 'default'}] {mode} {min(ts) * 1e3:.2f} ms  sweeps {sweeps}  {min(ts) / sweeps * 1e6:.3f} us/sweep  "
-          f"identical: {same}", flush=True)
+          f"identical: {same}  plan {pl['shape']} R={pl['R']} G={pl['G']} C={pl['C']} spt={pl['spt']}", flush=True)
     if os.environ.get("STAMPS"):
         os.environ["IRLMX_STAMPS"] = "1"
         call(); torch.cuda.synchronize()
