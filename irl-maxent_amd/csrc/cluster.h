@@ -54,6 +54,7 @@ struct ClusterArgs {
   int n_resident;          // workgroups of this launch that must run at once (coresident())
   unsigned long long gather_ticks;  // exchange timeout (s_memrealtime ticks; kGatherTicks unless a test shortens it)
   int test_drop;           // tests only (IRLMX_TEST_DROP_TILE): this workgroup leaves after the rendezvous, else -1
+  int eager_summary;       // A/B and tests (IRLMX_EAGER_SUMMARY=1): wait for every tile's summary every block
   unsigned long long* stamps;  // optional [grid][8] phase cycle counters (IRLMX_STAMPS=1), else null
   double* out;             // forward: svf [B][S]; backward: pi [B][S][A]
   int64_t* iters;

@@ -702,13 +702,11 @@ __global__ void __launch_bounds__(NT) cluster_kernel(ClusterArgs a) {
     bool ok = true;
     constexpr int GPT = PAIR ? kGatherPerThread : 1;  // ghost granules in flight per thread
     // Every tile's summary is waited for only when the block needs it (the
-    // forward's convergence bits, the backward's rescale blocks): between
-    // rescales a backward tile waits for its two neighbours' rows alone, not
-    // for the slowest of the instance's C tiles.
-#ifndef IRLMX_LAZY_SUMMARY
-#define IRLMX_LAZY_SUMMARY 1
-#endif
-    const bool need_summary = !IRLMX_LAZY_SUMMARY || MODE == kModeFwd || resc;
+    // forward's convergence bits, the backward's rescale blocks -- resc is the
+    // same in every tile of an instance): between rescales a backward tile
+    // waits for its two neighbours' rows alone, not for the slowest of the
+    // instance's C tiles.  (a.eager_summary: every block, for A/B tests.)
+    const bool need_summary = a.eager_summary || MODE == kModeFwd || resc;
     auto gather = [&]() {
       for (int k0 = 0; k0 < max(ng, 1); k0 += GPT * NT) {
         unsigned off[GPT + 1];
@@ -1092,6 +1090,7 @@ int cluster_run(int mode, const ClusterPlan& plan, ClusterArgs a, int B, hipStre
   // only): one workgroup leaves after the rendezvous, so its neighbours' exchange
   // times out (after the shortened limit) and the call takes the rerun path
   a.test_drop = env_int("IRLMX_TEST_DROP_TILE", -1);
+  a.eager_summary = env_int("IRLMX_EAGER_SUMMARY", 0) ? 1 : 0;
   const int tmo_ms = env_int("IRLMX_TEST_EXCHANGE_TIMEOUT_MS", 0);
   a.gather_ticks = tmo_ms > 0 ? (unsigned long long)tmo_ms * 100000ull : kGatherTicks;
   for (int b0 = 0; b0 < B; b0 += p.per_launch) {

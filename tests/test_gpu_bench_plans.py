@@ -249,3 +249,22 @@ def test_config4_full_vectors_plan_independent(dev):
         full.update(svf_f)
         alone.update(svf_a)
         assert torch.equal(full.theta[pick], alone.theta), (step, "theta")
+
+
+@pytest.mark.parametrize("size,B", [(128, 4), (256, 2)])
+def test_backward_lazy_summary_bit_identical(dev, monkeypatch, size, B):
+    """Backward tiles wait for every tile's block summary only on rescale blocks
+    (cluster.hip, need_summary); with IRLMX_EAGER_SUMMARY=1 every block waits
+    for all C tiles.  Both give the same policy bit for bit, on multi-tile plans
+    with rescaling active (random rewards up to 1.5)."""
+    from irlmx import DeviceMDP, ops
+    S = size * size
+    mdp = DeviceMDP.icy_gridworld(size, np.linspace(0.1, 0.3, B), device=dev)
+    assert ops.execution_plan(mdp, "backward")["C"] > 2
+    r = torch.as_tensor(np.random.default_rng(size).uniform(0.0, 1.5, (B, S)), device=dev)
+    tm = ops.terminal_mask([S - 1], S, batch=B, device=dev)
+    lazy = ops.backward_maxent(mdp, r, tm)
+    monkeypatch.setenv("IRLMX_EAGER_SUMMARY", "1")
+    eager = ops.backward_maxent(mdp, r, tm)
+    assert bool(torch.isfinite(lazy).all())
+    assert torch.equal(lazy, eager)
