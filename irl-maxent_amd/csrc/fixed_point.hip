@@ -296,6 +296,85 @@ __device__ inline int finish_status(double delta, double eps) {
   return delta > eps ? IRLMX_MAXITER : IRLMX_OK;
 }
 
+// The reference's fixed-point loops stop after the first sweep whose
+// max|x_new - x| is not > eps, NaN included (maxent.py:108, :335, solver.py:49).
+// run_deferred keeps that rule without a per-sweep reduction: each lane records
+// per sweep i "some |x_new - x| > eps" (bit i) and "some |x_new - x| is NaN"
+// (bit 32 + i) for its states (record_delta), and the workgroup ORs the bits
+// once per block of kDeferBlock sweeps.  If the block holds the stopping sweep
+// k, restore() puts the block-start state back (LDS and registers; save() took
+// it) and sweeps 0..k are replayed -- the same arithmetic, so the same bits.
+// sweep(it, pos, bits) runs one sweep from buffer parity it & 1 and records at
+// bit pos (the helpers put the barrier after it); slot[0..2] are zero on entry.
+// Returns the status (OK, NONFINITE, MAXITER); `it` counts the sweeps done.
+// One call site of sweep(), so it is inlined once.  run_each is the per-sweep
+// form for kernels whose registers have no room for the block bookkeeping: the
+// same bits, reduced every sweep with two ballots (no cross-lane shuffles).
+constexpr int kDeferBlock = 32;
+__device__ inline void record_delta(unsigned long long& bits, int pos, double d, double eps) {
+  bits |= ((d > eps) ? 1ull : 0ull) << pos;
+  bits |= ((d != d) ? 1ull : 0ull) << (32 + pos);
+}
+template <class Sweep, class Save, class Restore>
+__device__ __attribute__((always_inline)) inline int run_deferred(long long max_iter, unsigned long long* slot,
+                                                                  long long& it, Sweep&& sweep, Save&& save,
+                                                                  Restore&& restore) {
+  const int tid = threadIdx.x;
+  for (int blk = 0;; ++blk) {
+    save();
+    int nb = kDeferBlock;
+    if (max_iter > 0) nb = (int)min<long long>(nb, max_iter - it);
+    int k = -1;
+    unsigned nan = 0u;
+    for (int pass = 0; pass < 2; ++pass) {  // the block, then (stop inside it) the replay
+      unsigned long long bits = 0ull;
+      const int cnt = pass == 0 ? nb : k + 1;
+      for (int i = 0; i < cnt; ++i) {
+        sweep(it + i, i, bits);
+        __syncthreads();
+      }
+      if (pass == 1) break;
+      bits = wave_or_u64(bits);
+      if ((tid & (kWave - 1)) == 0 && bits) atomicOr(&slot[blk & 1], bits);
+      if (tid == 0) slot[(blk & 1) ^ 1] = 0ull;  // last read in the previous block, before this block's barriers
+      __syncthreads();
+      const unsigned long long all = slot[blk & 1];
+      const unsigned gt = (unsigned)all;
+      nan = (unsigned)(all >> 32);
+      const unsigned live = nb >= 32 ? 0xFFFFFFFFu : ((1u << nb) - 1u);
+      const unsigned stop = (~gt | nan) & live;
+      if (!stop) break;
+      k = __builtin_ctz(stop);
+      restore();
+    }
+    if (k >= 0) {
+      it += k + 1;
+      return ((nan >> k) & 1u) ? IRLMX_NONFINITE : IRLMX_OK;
+    }
+    it += nb;
+    if (max_iter > 0 && it >= max_iter) return IRLMX_MAXITER;
+  }
+}
+template <class Sweep>
+__device__ __attribute__((always_inline)) inline int run_each(long long max_iter, unsigned long long* slot,
+                                                              long long& it, Sweep&& sweep) {
+  const int tid = threadIdx.x;
+  for (int r3 = 0;; r3 = r3 == 2 ? 0 : r3 + 1) {
+    unsigned long long bits = 0ull;
+    sweep(it, 0, bits);
+    const unsigned long long w = (__builtin_amdgcn_ballot_w64((bits & 1ull) != 0ull) ? 1ull : 0ull) |
+                                 (__builtin_amdgcn_ballot_w64((bits >> 32) != 0ull) ? (1ull << 32) : 0ull);
+    if ((tid & (kWave - 1)) == 0 && w) atomicOr(&slot[r3], w);
+    if (tid == 0) slot[r3 == 2 ? 0 : r3 + 1] = 0ull;  // read two sweeps ago
+    __syncthreads();
+    const unsigned long long all = slot[r3];
+    ++it;
+    if (all >> 32) return IRLMX_NONFINITE;
+    if (!(all & 1ull)) return IRLMX_OK;
+    if (max_iter > 0 && it >= max_iter) return IRLMX_MAXITER;
+  }
+}
+
 // one barrier per sweep; LDS: two S-vectors + 3 convergence slots
 template <int SPT, int KMAX>
 __global__ void __launch_bounds__(1024) fwd_fused_kernel(FwdArgs a) {
@@ -306,6 +385,7 @@ __global__ void __launch_bounds__(1024) fwd_fused_kernel(FwdArgs a) {
   double* bufA = (double*)smem;
   double* bufB = bufA + S;
   unsigned long long* slot = (unsigned long long*)(bufB + S);
+  double* snap = (double*)(slot + 4);  // run_deferred's block-start state (LDS: the registers are taken)
 
   if (a.bad[b]) {  // non-finite policy: the reference yields NaN after one sweep
     for (int s = tid; s < S; s += nt) a.out[(size_t)b * S + s] = __longlong_as_double(0x7ff8000000000000LL);
@@ -336,12 +416,9 @@ __global__ void __launch_bounds__(1024) fwd_fused_kernel(FwdArgs a) {
   __syncthreads();
 
   long long it = 0;
-  int r3 = 0;
-  double delta = 0.0;
-  for (;;) {
+  auto sweep = [&](long long it, int pos, unsigned long long& bits) __attribute__((always_inline)) {
     const double* din = (it & 1) ? bufB : bufA;
     double* dout = (it & 1) ? bufA : bufB;
-    unsigned long long mx = 0ull;
 #pragma unroll
     for (int j = 0; j < SPT; ++j) {
       const int s = tid + j * nt;
@@ -352,27 +429,37 @@ __global__ void __launch_bounds__(1024) fwd_fused_kernel(FwdArgs a) {
           if (k < K) acc = fma(w[j][k], din[nb[j][k]], acc);
         const double nv = p0[j] + acc;
         dout[s] = nv;
-        const unsigned long long d = abs_bits(nv - cur[j]);
-        mx = d > mx ? d : mx;
+        record_delta(bits, pos, fabs(nv - cur[j]), a.eps);
         cur[j] = nv;
       }
     }
-    mx = wave_max_u64(mx);
-    if ((tid & (kWave - 1)) == 0 && mx) atomicMax(&slot[r3], mx);
-    if (tid == 0) slot[r3 == 2 ? 0 : r3 + 1] = 0ull;
-    __syncthreads();
-    delta = bits_double(slot[r3]);
-    r3 = r3 == 2 ? 0 : r3 + 1;
-    ++it;
-    if (!(delta > a.eps)) break;
-    if (a.max_iter > 0 && it >= a.max_iter) break;
+  };
+  // (the widest ELL rows fill the registers: per-sweep bits there)
+  int status;
+  if constexpr (SPT * KMAX < 32) {
+    status = run_deferred(
+        a.max_iter, slot, it, sweep,
+        [&]() {
+#pragma unroll
+          for (int j = 0; j < SPT; ++j)
+            if (tid + j * nt < S) snap[tid + j * nt] = cur[j];
+        },
+        [&]() {
+          double* d0 = (it & 1) ? bufB : bufA;
+#pragma unroll
+          for (int j = 0; j < SPT; ++j)
+            if (tid + j * nt < S) d0[tid + j * nt] = cur[j] = snap[tid + j * nt];
+          __syncthreads();
+        });
+  } else {
+    status = run_each(a.max_iter, slot, it, sweep);
   }
 #pragma unroll
   for (int j = 0; j < SPT; ++j) {
     const int s = tid + j * nt;
     if (s < S) a.out[(size_t)b * S + s] = cur[j];
   }
-  if (tid == 0) { a.iters[b] = it; a.status[b] = finish_status(delta, a.eps); }
+  if (tid == 0) { a.iters[b] = it; a.status[b] = status; }
 }
 
 struct BwdArgs {
@@ -789,18 +876,9 @@ __global__ void __launch_bounds__(kNpCachedThreads) fwd_numpy_order_cached_kerne
   __syncthreads();
   if (nf) bad[1] = 1;
   __syncthreads();
-  // Convergence deferred over blocks of kNpFwdBlock sweeps: each lane records
-  // per sweep i "some |d_ - d| > eps" (bit i) and "some |d_ - d| is NaN" (bit
-  // 32 + i) for its targets, and the workgroup ORs the bits once per block --
-  // no per-sweep max reduction (its six cross-lane steps were most of a
-  // sweep's latency).  The reference stops after the first sweep whose
-  // np.max|d_ - d| is not > eps, NaN included (maxent.py:108): if a block holds
-  // that sweep, the block-start state (kept in registers) goes back into LDS and
-  // the sweeps up to it are replayed -- the same arithmetic, so the same bits.
-  constexpr int kNpFwdBlock = 32;
+  // convergence deferred over blocks of sweeps, replay of the stopping block
+  // (run_deferred); the poison flags bad[] are part of the block-start state
   long long it = 0;
-  int status = IRLMX_OK;
-  // one sweep from buffer parity it & 1, its bits recorded at position pos
   auto sweep = [&](long long it, int pos, unsigned long long& bits) __attribute__((always_inline)) {
     const double* d = ((it & 1) ? buf1 : buf0);
     double* dn = ((it & 1) ? buf0 : buf1);
@@ -846,59 +924,30 @@ __global__ void __launch_bounds__(kNpCachedThreads) fwd_numpy_order_cached_kerne
       const double nv = __dadd_rn(p0t[j], v);  // maxent.py:110
       dn[t] = nv;
       nfo |= !isfinite(nv);
-      const double dd = fabs(nv - d[t]);
-      bits |= ((dd > a.eps) ? 1ull : 0ull) << pos;
-      bits |= ((dd != dd) ? 1ull : 0ull) << (32 + pos);
+      record_delta(bits, pos, fabs(nv - d[t]), a.eps);
     }
     if (nfo) bad[it & 1] = 1;
-    __syncthreads();
   };
-  for (int blk = 0;; ++blk) {
-    double keep[TPT];
-    const double* d0 = ((it & 1) ? buf1 : buf0);
+  double keep[TPT];
+  int bad0 = 0, bad1 = 0;
+  const int status = run_deferred(
+      a.max_iter, slot, it, sweep,
+      [&]() {
+        const double* d0 = ((it & 1) ? buf1 : buf0);
 #pragma unroll
-    for (int j = 0; j < TPT; ++j) keep[j] = tid + j * nt < S ? d0[tid + j * nt] : 0.0;
-    const int bad0 = bad[0], bad1 = bad[1];
-    int nb = kNpFwdBlock;
-    if (a.max_iter > 0) nb = (int)min<long long>(nb, a.max_iter - it);
-    // pass 0: the block with its bits; pass 1 (the stop inside the block): the
-    // replay from the block start up to the stopping sweep k (one call site of
-    // the sweep, so it is inlined once)
-    int k = -1;
-    unsigned nan = 0u;
-    for (int pass = 0; pass < 2; ++pass) {
-      unsigned long long bits = 0ull;
-      const int cnt = pass == 0 ? nb : k + 1;
-      for (int i = 0; i < cnt; ++i) sweep(it + i, i, bits);
-      if (pass == 1) break;
-      bits = wave_or_u64(bits);
-      if ((tid & (kWave - 1)) == 0 && bits) atomicOr(&slot[blk & 1], bits);
-      if (tid == 0) slot[(blk & 1) ^ 1] = 0ull;  // last read in the previous block, before this block's barriers
-      __syncthreads();
-      const unsigned long long all = slot[blk & 1];
-      const unsigned gt = (unsigned)all;
-      nan = (unsigned)(all >> 32);
-      const unsigned live = nb >= 32 ? 0xFFFFFFFFu : ((1u << nb) - 1u);
-      const unsigned stop = (~gt | nan) & live;
-      if (!stop) break;
-      // the stopping sweep is inside this block: back to its start
-      k = __builtin_ctz(stop);
-      double* d0w = ((it & 1) ? buf1 : buf0);
+        for (int j = 0; j < TPT; ++j) keep[j] = tid + j * nt < S ? d0[tid + j * nt] : 0.0;
+        bad0 = bad[0];
+        bad1 = bad[1];
+      },
+      [&]() {
+        double* d0w = ((it & 1) ? buf1 : buf0);
 #pragma unroll
-      for (int j = 0; j < TPT; ++j)
-        if (tid + j * nt < S) d0w[tid + j * nt] = keep[j];
-      __syncthreads();  // every lane past its reads of bad[] before they are restored
-      if (tid == 0) { bad[0] = bad0; bad[1] = bad1; }
-      __syncthreads();
-    }
-    if (k >= 0) {
-      it += k + 1;
-      status = ((nan >> k) & 1u) ? IRLMX_NONFINITE : IRLMX_OK;
-      break;
-    }
-    it += nb;
-    if (a.max_iter > 0 && it >= a.max_iter) { status = IRLMX_MAXITER; break; }
-  }
+        for (int j = 0; j < TPT; ++j)
+          if (tid + j * nt < S) d0w[tid + j * nt] = keep[j];
+        __syncthreads();  // every lane past its reads of bad[] before they are restored
+        if (tid == 0) { bad[0] = bad0; bad[1] = bad1; }
+        __syncthreads();
+      });
   for (int t = tid; t < S; t += nt) a.svf[(size_t)b * S + t] = ((it & 1) ? buf1 : buf0)[t];
   if (tid == 0) {
     a.iters[b] = it;
@@ -1135,6 +1184,7 @@ __device__ __forceinline__ void bellman_fused_body(const SoftArgs& a, unsigned c
   double* bufA = (double*)smem;
   double* bufB = bufA + S;
   unsigned long long* slot = (unsigned long long*)(bufB + S);
+  double* snap = (double*)(slot + 4);  // run_deferred's block-start state (LDS: the registers are taken)
 
   int nb[SPT][KMAX];
   double r[SPT], phi[SPT], cur[SPT];
@@ -1160,32 +1210,39 @@ __device__ __forceinline__ void bellman_fused_body(const SoftArgs& a, unsigned c
   __syncthreads();
 
   long long it = 0;
-  int r3 = 0;
-  double delta = 0.0;
-  for (;;) {
+  auto sweep = [&](long long it, int pos, unsigned long long& bits) __attribute__((always_inline)) {
     const double* vin = (it & 1) ? bufB : bufA;
     double* vout = (it & 1) ? bufA : bufB;
-    unsigned long long mx = 0ull;
 #pragma unroll
     for (int j = 0; j < SPT; ++j) {
       const int s = tid + j * nt;
       if (s < S) {
         const double v = bellman_update<SOFT, KMAX, true>(a, b, s, nb[j], vin, r[j], phi[j]);
         vout[s] = v;
-        const unsigned long long d = abs_bits(v - cur[j]);
-        mx = d > mx ? d : mx;
+        record_delta(bits, pos, fabs(v - cur[j]), a.eps);
         cur[j] = v;
       }
     }
-    mx = wave_max_u64(mx);
-    if ((tid & (kWave - 1)) == 0 && mx) atomicMax(&slot[r3], mx);
-    if (tid == 0) slot[r3 == 2 ? 0 : r3 + 1] = 0ull;
-    __syncthreads();
-    delta = bits_double(slot[r3]);
-    r3 = r3 == 2 ? 0 : r3 + 1;
-    ++it;
-    if (!(delta > a.eps)) break;
-    if (a.max_iter > 0 && it >= a.max_iter) break;
+  };
+  // (the widest rows fill the registers: per-sweep bits there)
+  int status;
+  if constexpr (SPT * KMAX < 32) {
+    status = run_deferred(
+        a.max_iter, slot, it, sweep,
+        [&]() {
+#pragma unroll
+          for (int j = 0; j < SPT; ++j)
+            if (tid + j * nt < S) snap[tid + j * nt] = cur[j];
+        },
+        [&]() {
+          double* v0w = (it & 1) ? bufB : bufA;
+#pragma unroll
+          for (int j = 0; j < SPT; ++j)
+            if (tid + j * nt < S) v0w[tid + j * nt] = cur[j] = snap[tid + j * nt];
+          __syncthreads();
+        });
+  } else {
+    status = run_each(a.max_iter, slot, it, sweep);
   }
   const double* vold = (it & 1) ? bufA : bufB;  // input of the last sweep
 #pragma unroll
@@ -1198,7 +1255,7 @@ __device__ __forceinline__ void bellman_fused_body(const SoftArgs& a, unsigned c
   }
   if (tid == 0) {
     if (a.iters) a.iters[b] = it;
-    a.status[b] = finish_status(delta, a.eps);
+    a.status[b] = status;
   }
 }
 
@@ -1297,12 +1354,10 @@ __global__ void __launch_bounds__(kNpCachedThreads) bellman_numpy_order_cached_k
   for (int s = tid; s < S; s += nt) buf0[s] = v0;
   if (tid < 3) slot[tid] = 0ull;
   __syncthreads();
-  // convergence deferred over blocks of 32 sweeps, replay of the stopping
-  // block: as in fwd_numpy_order_cached_kernel (the stop after the first sweep
-  // whose max|v_new - v| is not > eps, NaN included: solver.py:49, maxent.py:335)
-  constexpr int kNpBlock = 32;
+  // convergence deferred over blocks of sweeps, replay of the stopping block
+  // (run_deferred: the stop after the first sweep whose max|v_new - v| is not
+  // > eps, NaN included -- solver.py:49, maxent.py:335)
   long long it = 0;
-  int status = IRLMX_OK;
   auto sweep = [&](long long it, int pos, unsigned long long& bits) __attribute__((always_inline)) {
     const double* vin = ((it & 1) ? buf1 : buf0);
     double* vout = ((it & 1) ? buf0 : buf1);
@@ -1327,51 +1382,24 @@ __global__ void __launch_bounds__(kNpCachedThreads) bellman_numpy_order_cached_k
       }
       if (!SOFT) v = __dadd_rn(rr[j], a.average ? v / (double)A : v);  // solver.py:47 / :99
       vout[s] = v;
-      const double d = fabs(v - vin[s]);
-      bits |= ((d > a.eps) ? 1ull : 0ull) << pos;
-      bits |= ((d != d) ? 1ull : 0ull) << (32 + pos);
+      record_delta(bits, pos, fabs(v - vin[s]), a.eps);
     }
-    __syncthreads();
   };
-  for (int blk = 0;; ++blk) {
-    double keep[TPT];
-    const double* v0p = ((it & 1) ? buf1 : buf0);
+  double keep[TPT];
+  const int status = run_deferred(
+      a.max_iter, slot, it, sweep,
+      [&]() {
+        const double* v0p = ((it & 1) ? buf1 : buf0);
 #pragma unroll
-    for (int j = 0; j < TPT; ++j) keep[j] = tid + j * nt < S ? v0p[tid + j * nt] : 0.0;
-    int nb = kNpBlock;
-    if (a.max_iter > 0) nb = (int)min<long long>(nb, a.max_iter - it);
-    int k = -1;
-    unsigned nan = 0u;
-    for (int pass = 0; pass < 2; ++pass) {  // the block, then (stop inside it) the replay
-      unsigned long long bits = 0ull;
-      const int cnt = pass == 0 ? nb : k + 1;
-      for (int i = 0; i < cnt; ++i) sweep(it + i, i, bits);
-      if (pass == 1) break;
-      bits = wave_or_u64(bits);
-      if ((tid & (kWave - 1)) == 0 && bits) atomicOr(&slot[blk & 1], bits);
-      if (tid == 0) slot[(blk & 1) ^ 1] = 0ull;  // last read in the previous block, before this block's barriers
-      __syncthreads();
-      const unsigned long long all = slot[blk & 1];
-      const unsigned gt = (unsigned)all;
-      nan = (unsigned)(all >> 32);
-      const unsigned live = nb >= 32 ? 0xFFFFFFFFu : ((1u << nb) - 1u);
-      const unsigned stop = (~gt | nan) & live;
-      if (!stop) break;
-      k = __builtin_ctz(stop);
-      double* v0w = ((it & 1) ? buf1 : buf0);
+        for (int j = 0; j < TPT; ++j) keep[j] = tid + j * nt < S ? v0p[tid + j * nt] : 0.0;
+      },
+      [&]() {
+        double* v0w = ((it & 1) ? buf1 : buf0);
 #pragma unroll
-      for (int j = 0; j < TPT; ++j)
-        if (tid + j * nt < S) v0w[tid + j * nt] = keep[j];
-      __syncthreads();
-    }
-    if (k >= 0) {
-      it += k + 1;
-      status = ((nan >> k) & 1u) ? IRLMX_NONFINITE : IRLMX_OK;
-      break;
-    }
-    it += nb;
-    if (a.max_iter > 0 && it >= a.max_iter) { status = IRLMX_MAXITER; break; }
-  }
+        for (int j = 0; j < TPT; ++j)
+          if (tid + j * nt < S) v0w[tid + j * nt] = keep[j];
+        __syncthreads();
+      });
   const double* vold = ((it & 1) ? buf0 : buf1);  // input of the last sweep
   const double* vnew = ((it & 1) ? buf1 : buf0);
 #pragma unroll
@@ -2239,7 +2267,8 @@ static bool use_fused(const Model& m, int op) {
   return fused_shape(m, op, &f);
 }
 
-static size_t fused_lds(const Model& m) { return 2 * (size_t)m.S * sizeof(double) + 4 * sizeof(unsigned long long); }
+// two S-vectors, the convergence slots and (run_deferred) the block-start snapshot
+static size_t fused_lds(const Model& m) { return 3 * (size_t)m.S * sizeof(double) + 4 * sizeof(unsigned long long); }
 
 // Kernel-pointer getters: only the (SPT, KMAX) pairs fused_pair_ok() admits
 // are instantiated.
