@@ -394,14 +394,18 @@ __global__ void __launch_bounds__(NT) cluster_kernel(ClusterArgs a) {
       double side[2][2];  // [top, bottom][left, right]
       // (which: 1 = the row above, 2 = the row below, 3 = both; sync: the barrier first)
 #ifndef IRLMX_PIN_BARRIER
-#define IRLMX_PIN_BARRIER 0
+#define IRLMX_PIN_BARRIER -1
 #endif
+      // Column pairs: keep the instruction scheduler from moving the interior
+      // rows' FMAs across the barrier (it hoisted the barrier to the top of the
+      // loop body; config 3 backward 24.4 -> 23.0 ms on one box).  Column
+      // quads are faster unpinned (267.6 vs 273.6 ms at config 4).
+      // (IRLMX_PIN_BARRIER: -1 pairs only, 0 never, 1 always.)
+      constexpr bool kPin = IRLMX_PIN_BARRIER < 0 ? CPL == 2 : IRLMX_PIN_BARRIER != 0;
       auto edges_in = [&](int which = 3, bool sync = true) {
-        // (IRLMX_PIN_BARRIER: keep the instruction scheduler from moving the
-        // interior rows' FMAs across the barrier)
-        if (IRLMX_PIN_BARRIER && sync) __builtin_amdgcn_sched_barrier(0);
+        if (kPin && sync) __builtin_amdgcn_sched_barrier(0);
         if (sync) __syncthreads();
-        if (IRLMX_PIN_BARRIER && sync) __builtin_amdgcn_sched_barrier(0);
+        if (kPin && sync) __builtin_amdgcn_sched_barrier(0);
         const double2* t = bnd_at(i & 1, bb, 1);
         const double2* u = bnd_at(i & 1, bb + 2, 0);
 #pragma unroll

@@ -434,7 +434,7 @@ __global__ void __launch_bounds__(1024) fwd_fused_kernel(FwdArgs a) {
       }
     }
   };
-  // (the widest ELL rows fill the registers: per-sweep bits there)
+  // (the widest ELL rows fill the registers: the per-sweep reduction there)
   int status;
   if constexpr (SPT * KMAX < 32) {
     status = run_deferred(
@@ -452,7 +452,39 @@ __global__ void __launch_bounds__(1024) fwd_fused_kernel(FwdArgs a) {
           __syncthreads();
         });
   } else {
-    status = run_each(a.max_iter, slot, it, sweep);
+    // the per-sweep max reduction (these kernels sit at the register limit)
+    int r3 = 0;
+    double delta = 0.0;
+    for (;;) {
+      const double* din = (it & 1) ? bufB : bufA;
+      double* dout = (it & 1) ? bufA : bufB;
+      unsigned long long mx = 0ull;
+#pragma unroll
+      for (int j = 0; j < SPT; ++j) {
+        const int s = tid + j * nt;
+        if (s < S) {
+          double acc = 0.0;
+#pragma unroll
+          for (int k = 0; k < KMAX; ++k)
+            if (k < K) acc = fma(w[j][k], din[nb[j][k]], acc);
+          const double nv = p0[j] + acc;
+          dout[s] = nv;
+          const unsigned long long d = abs_bits(nv - cur[j]);
+          mx = d > mx ? d : mx;
+          cur[j] = nv;
+        }
+      }
+      mx = wave_max_u64(mx);
+      if ((tid & (kWave - 1)) == 0 && mx) atomicMax(&slot[r3], mx);
+      if (tid == 0) slot[r3 == 2 ? 0 : r3 + 1] = 0ull;
+      __syncthreads();
+      delta = bits_double(slot[r3]);
+      r3 = r3 == 2 ? 0 : r3 + 1;
+      ++it;
+      if (!(delta > a.eps)) break;
+      if (a.max_iter > 0 && it >= a.max_iter) break;
+    }
+    status = finish_status(delta, a.eps);
   }
 #pragma unroll
   for (int j = 0; j < SPT; ++j) {
@@ -890,7 +922,7 @@ __global__ void __launch_bounds__(kNpCachedThreads) fwd_numpy_order_cached_kerne
       if (t >= S) continue;
       double dv[kStencilK];
 #pragma unroll
-      for (int i = 0; i < kStencilK; ++i) dv[i] = i < n[j] ? d[src[j][i]] : 0.0;
+      for (int i = 0; i < kStencilK; ++i) dv[i] = d[src[j][i]];  // (unused entries: src 0, selected away below)
       // all actions' chains side by side, branch-free (the entries' kinds differ
       // between lanes): every step computes its candidates and selects, so the
       // four independent chains interleave instead of diverging
@@ -904,12 +936,17 @@ __global__ void __launch_bounds__(kNpCachedThreads) fwd_numpy_order_cached_kerne
         const bool flush = open && (kd == 1 || kd == 2);
 #pragma unroll
         for (int act = 0; act < kNpCachedMaxActions; ++act) {
+          // every candidate computed, then selected: a conditional operator
+          // around an arithmetic call compiles to an exec-mask branch per step
           const double vv = val[j][act][i];
           const double x = __dmul_rn(pw[j][act][i], dv[i]);  // maxent.py:109
-          const double o1 = flush ? __dadd_rn(out[act], c[act]) : out[act];
+          const double oc = __dadd_rn(out[act], c[act]);
+          const double o1 = flush ? oc : out[act];
           const double cf = fma(vv, x, kd == 1 ? 0.0 : c[act]);
+          const double f3 = fma(vv, x, out[act]);
+          const double a2 = __dadd_rn(o1, __dmul_rn(vv, x));
           c[act] = (kd == 0 || kd == 1) ? cf : c[act];
-          out[act] = kd == 3 ? fma(vv, x, out[act]) : (kd == 2 ? __dadd_rn(o1, __dmul_rn(vv, x)) : o1);
+          out[act] = kd == 3 ? f3 : (kd == 2 ? a2 : o1);
         }
         open = kd == 1 ? true : (kd == 2 ? false : open);
       }
@@ -917,7 +954,8 @@ __global__ void __launch_bounds__(kNpCachedThreads) fwd_numpy_order_cached_kerne
 #pragma unroll
       for (int act = 0; act < kNpCachedMaxActions; ++act) {
         if (act >= A) break;
-        const double o = open ? __dadd_rn(out[act], c[act]) : out[act];
+        const double oc = __dadd_rn(out[act], c[act]);
+        const double o = open ? oc : out[act];
         const double y = poisoned ? kNaN : o;
         v = act == 0 ? y : __dadd_rn(v, y);  // np.array(d_).sum(axis=0)
       }
@@ -1224,9 +1262,11 @@ __device__ __forceinline__ void bellman_fused_body(const SoftArgs& a, unsigned c
       }
     }
   };
-  // (the widest rows fill the registers: per-sweep bits there)
+  // (VI converges in tens of sweeps, where a block's overshoot and replay cost
+  // more than a reduction per sweep; the widest rows fill the registers: per-
+  // sweep bits there too)
   int status;
-  if constexpr (SPT * KMAX < 32) {
+  if constexpr (SOFT && SPT * KMAX < 32) {
     status = run_deferred(
         a.max_iter, slot, it, sweep,
         [&]() {
@@ -1385,21 +1425,27 @@ __global__ void __launch_bounds__(kNpCachedThreads) bellman_numpy_order_cached_k
       record_delta(bits, pos, fabs(v - vin[s]), a.eps);
     }
   };
+  // (VI: a reduction per sweep, as in bellman_fused_body)
   double keep[TPT];
-  const int status = run_deferred(
-      a.max_iter, slot, it, sweep,
-      [&]() {
-        const double* v0p = ((it & 1) ? buf1 : buf0);
+  int status;
+  if constexpr (SOFT) {
+    status = run_deferred(
+        a.max_iter, slot, it, sweep,
+        [&]() {
+          const double* v0p = ((it & 1) ? buf1 : buf0);
 #pragma unroll
-        for (int j = 0; j < TPT; ++j) keep[j] = tid + j * nt < S ? v0p[tid + j * nt] : 0.0;
-      },
-      [&]() {
-        double* v0w = ((it & 1) ? buf1 : buf0);
+          for (int j = 0; j < TPT; ++j) keep[j] = tid + j * nt < S ? v0p[tid + j * nt] : 0.0;
+        },
+        [&]() {
+          double* v0w = ((it & 1) ? buf1 : buf0);
 #pragma unroll
-        for (int j = 0; j < TPT; ++j)
-          if (tid + j * nt < S) v0w[tid + j * nt] = keep[j];
-        __syncthreads();
-      });
+          for (int j = 0; j < TPT; ++j)
+            if (tid + j * nt < S) v0w[tid + j * nt] = keep[j];
+          __syncthreads();
+        });
+  } else {
+    status = run_each(a.max_iter, slot, it, sweep);
+  }
   const double* vold = ((it & 1) ? buf0 : buf1);  // input of the last sweep
   const double* vnew = ((it & 1) ? buf1 : buf0);
 #pragma unroll
