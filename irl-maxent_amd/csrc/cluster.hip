@@ -467,7 +467,11 @@ __global__ void __launch_bounds__(NT) cluster_kernel(ClusterArgs a) {
       // arrival), the rest while the edge reads after the barrier are in flight.
       constexpr int step = CPL == 2 ? 2 : 1;
       constexpr int n_int = RW >= 3 ? (RW - 2 + step - 1) / step : 0;
-      constexpr int kPre = (n_int + 1) / 2;
+#ifndef IRLMX_KPRE
+#define IRLMX_KPRE -1
+#endif
+      // (IRLMX_KPRE >= 0: experiments, interior steps before the barrier)
+      constexpr int kPre = IRLMX_KPRE >= 0 ? (IRLMX_KPRE < n_int ? IRLMX_KPRE : n_int) : (n_int + 1) / 2;
       // IRLMX_QUAD_LAZY_ABOVE (quads): the row below is read at the barrier, the
       // row above only before the band's top row, so the two edge rows are never
       // live together (four doubles less register pressure; the hot loop has no
