@@ -24,6 +24,13 @@ constexpr int kSoloBwdT = 256;     // backward sweeps per block of a solo tile (
 #endif
 constexpr int kRescaleEvery = IRLMX_RESCALE_EVERY;  // backward: max blocks between rescales
 constexpr size_t kMaxLdsBytes = 160 * 1024;  // LDS per CU (one workgroup per CU)
+// Tile-summary granule slots per instance, indexed by block % kSumSlots.  A
+// backward tile reads the other tiles' summaries only on rescale blocks (at
+// most kRescaleEvery apart), so between two such blocks a tile can run ahead
+// of a distant tile by up to kRescaleEvery blocks; its summary for block m + 4
+// must not land in the slot a slow tile is still polling for block m.
+constexpr int kSumSlots = 8;
+static_assert(kSumSlots > kRescaleEvery, "summary slots must outlast the rescale period");
 constexpr size_t kClusterStaticLds = 128;     // cluster_kernel's own __shared__ variables (resident flag, stamps)
 constexpr int kModeFwd = 0;
 constexpr int kModeBwd = 1;
@@ -47,7 +54,7 @@ struct ClusterArgs {
   long long n_sweeps;      // backward: collapsed sweeps (2S - 1)
   int rescale;
   unsigned long long* gran;   // [B][2][S] x 16-byte tagged granule pairs (halo rows)
-  unsigned long long* sgran;  // [B][3][H] x 16-byte tagged granule pairs (tile summaries, XCC ids)
+  unsigned long long* sgran;  // [B][kSumSlots + 1][H] x 16-byte tagged granule pairs (tile summaries, XCC ids)
   int xcd_group;           // number the tiles of an instance within one XCD group
   unsigned salt;           // per-launch granule tag salt
   int* err;                // [0]: exchange timeout (1), non-finite (2), not co-resident (4); [1..2]: rendezvous

@@ -357,6 +357,17 @@ __global__ void __launch_bounds__(NT) cluster_kernel(ClusterArgs a) {
   // band edge row e (0: top, 1: bottom) of band slot `band` (0 and NB + 1 are
   // the zero bands) in parity buffer `par`
   auto bnd_at = [&](int par, int band, int e) { return bnd + ((((size_t)par * (NB + 2) + band) * 2 + e) * HW + cp) * QW; };
+  // kSplitEdges (column pairs): the same storage per edge row as two arrays of
+  // HW doubles (column 0, column 1), so that the side reads -- the neighbour
+  // lanes' last / first column -- are 8-byte strided (no bank conflicts; the
+  // double2 form reads them at a 16-byte stride)
+#ifndef IRLMX_SPLIT_EDGES
+#define IRLMX_SPLIT_EDGES 0
+#endif
+  constexpr bool kSplitEdges = kLdsSides && IRLMX_SPLIT_EDGES;
+  auto edge_row = [&](int par, int band, int e) {
+    return reinterpret_cast<double*>(bnd + (((size_t)par * (NB + 2) + band) * 2 + e) * HW * QW);
+  };
   auto cols_sweep = [&](const double (&src)[COLS ? SPT : 1], double (&dst)[COLS ? SPT : 1], int i,
                         unsigned& flags) {
     if constexpr (COLS) {
@@ -365,7 +376,12 @@ __global__ void __launch_bounds__(NT) cluster_kernel(ClusterArgs a) {
       auto account = [&](int j, double nv, double self) {
         if (MODE == kModeFwd && ((ob >> j) & 1u)) dmax = fmax(dmax, fabs(nv - self));
       };
-      {  // band edge rows (old values) out
+      if constexpr (kSplitEdges) {  // band edge rows (old values) out: column 0 / column 1 arrays
+        double* t = edge_row(i & 1, bb + 1, 0);
+        double* u = edge_row(i & 1, bb + 1, 1);
+        t[cp] = src[0]; t[HW + cp] = src[1];
+        u[cp] = src[SPT - 2]; u[HW + cp] = src[SPT - 1];
+      } else {  // band edge rows (old values) out
         double2* t = bnd_at(i & 1, bb + 1, 0);
         double2* u = bnd_at(i & 1, bb + 1, 1);
 #pragma unroll
@@ -406,6 +422,19 @@ __global__ void __launch_bounds__(NT) cluster_kernel(ClusterArgs a) {
         if (kPin && sync) __builtin_amdgcn_sched_barrier(0);
         if (sync) __syncthreads();
         if (kPin && sync) __builtin_amdgcn_sched_barrier(0);
+        if constexpr (kSplitEdges) {
+          const double* t = edge_row(i & 1, bb, 1);
+          const double* u = edge_row(i & 1, bb + 2, 0);
+          if (which & 1) { above[0] = t[cp]; above[1] = t[HW + cp]; }
+          if (which & 2) { below[0] = u[cp]; below[1] = u[HW + cp]; }
+#pragma unroll
+          for (int e = 0; e < 2; ++e) {  // left: column 1 of lane cp - 1; right: column 0 of lane cp + 1
+            const double* o = edge_row(i & 1, bb + 1, e);
+            side[e][0] = o[HW + cp - 1];
+            side[e][1] = o[cp + 1];
+          }
+          return;
+        }
         const double2* t = bnd_at(i & 1, bb, 1);
         const double2* u = bnd_at(i & 1, bb + 2, 0);
 #pragma unroll
@@ -500,9 +529,10 @@ __global__ void __launch_bounds__(NT) cluster_kernel(ClusterArgs a) {
   };
 
   // Halo exchange in tagged granules (cluster.h): this instance's region of
-  // a.gran is [2 parities][S states] x 16 B, of a.sgran [2][H tiles] x 16 B.
+  // a.gran is [2 parities][S states] x 16 B, of a.sgran [kSumSlots + 1][H tiles] x 16 B
+  // (summaries by block % kSumSlots, then the XCC ids).
   const Gran rg = gran_rsrc(a.gran + (size_t)inst * 4 * S, 32u * (unsigned)S);
-  const Gran rs = gran_rsrc(a.sgran + (size_t)inst * 6 * a.H, 48u * (unsigned)a.H);
+  const Gran rs = gran_rsrc(a.sgran + (size_t)inst * 2 * (kSumSlots + 1) * a.H, 16u * (kSumSlots + 1) * (unsigned)a.H);
   const int ng0 = own0, ng = own0 + (E - own1);  // ghost states: [0, own0) and [own1, E)
   const unsigned salt = (a.salt & 0xFFFu) << 20;  // per call: a stale granule of an earlier call never matches
   // Hand-off store form: write-through (sc1) in general; plain stores (kept in
@@ -514,13 +544,13 @@ __global__ void __launch_bounds__(NT) cluster_kernel(ClusterArgs a) {
     asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
     xcc &= 0xFu;
     const unsigned htag = salt | 0xFFFFFu;
-    if (tid == 0) gran_store(rs, (2u * (unsigned)a.H + (unsigned)tile) * 16u, xcc, htag, false);
+    if (tid == 0) gran_store(rs, ((unsigned)kSumSlots * (unsigned)a.H + (unsigned)tile) * 16u, xcc, htag, false);
     bool ok = true;
     if (tid < kWave) {
       unsigned long long diff = 0ull;
       for (int t0 = 0; t0 < a.C; t0 += kWave) {
         unsigned long long v[1] = {xcc};
-        unsigned off[1] = {(2u * (unsigned)a.H + (unsigned)(t0 + tid)) * 16u};
+        unsigned off[1] = {((unsigned)kSumSlots * (unsigned)a.H + (unsigned)(t0 + tid)) * 16u};
         ok &= gran_gather<1>(rs, rs, off, t0 + tid < a.C ? 1u : 0u, htag, v, a.gather_ticks);
         diff |= v[0] ^ xcc;
       }
@@ -679,7 +709,7 @@ __global__ void __launch_bounds__(NT) cluster_kernel(ClusterArgs a) {
     if (stamps) { const unsigned long long t = stamp_now(); st_acc[6] += t - ts; }
     __syncthreads();  // the tile summary in red32[m & 1] (and COLS: the staged rows) complete
     if (!solo) {
-      if (tid == 0) gran_store(rs, ((unsigned)(m & 1) * (unsigned)a.H + (unsigned)tile) * 16u, red32[m & 1], tag, plain);
+      if (tid == 0) gran_store(rs, ((unsigned)(m % kSumSlots) * (unsigned)a.H + (unsigned)tile) * 16u, red32[m & 1], tag, plain);
       if constexpr (COLS && CPL == 2) {
         store_rows();
       } else if constexpr (COLS) {
@@ -727,7 +757,7 @@ __global__ void __launch_bounds__(NT) cluster_kernel(ClusterArgs a) {
           off[i] = (gpar + (unsigned)(base + ls[i])) * 16u;
           want |= (k < ng ? 1u : 0u) << i;
         }
-        off[GPT] = ((unsigned)(m & 1) * (unsigned)a.H + (unsigned)tid) * 16u;
+        off[GPT] = ((unsigned)(m % kSumSlots) * (unsigned)a.H + (unsigned)tid) * 16u;
         want |= (k0 == 0 && tid < a.C && need_summary ? 1u : 0u) << GPT;
         unsigned long long v[GPT + 1];
         ok &= gran_gather<GPT + 1>(rg, rs, off, want, tag, v, a.gather_ticks);

@@ -176,11 +176,11 @@ static Ws carve(const Model& m, int op, void* base) {
   const bool gr = sweep && grid_plan(m, op, &gp);
   DenseGridPlan dp{0, 0, 0, 0};
   const bool dg = sweep && dense_grid(m, op, &dp);
-  // cluster halo exchange: [B][2][S] and [B][3][H] 16-byte granule pairs;
+  // cluster halo exchange: [B][2][S] and [B][kSumSlots + 1][H] 16-byte granule pairs;
   // grid shape: [B][3][S] value and [B][3][bpi] block-delta granules;
   // dense grid shape: [B][2][S] value and [B][bpi] XCC-id granules
   w.gran = (unsigned long long*)take(cl || dg ? 2 * B * S * 16 : (gr ? 3 * B * S * 16 : 0));
-  w.sgran = (unsigned long long*)take(cl ? 3 * B * (size_t)m.H * 16
+  w.sgran = (unsigned long long*)take(cl ? (kSumSlots + 1) * B * (size_t)m.H * 16
                                          : (gr ? 4 * B * (size_t)gp.bpi * 16 : (dg ? B * (size_t)dp.bpi * 16 : 0)));
   w.growth = (unsigned long long*)take(cl ? B * sizeof(unsigned long long) : 0);
   w.err = (int*)take(cl || gr || dg ? 4 * sizeof(int) : 0);
