@@ -710,7 +710,10 @@ __global__ void __launch_bounds__(NT) cluster_kernel(ClusterArgs a) {
     __syncthreads();  // the tile summary in red32[m & 1] (and COLS: the staged rows) complete
     if (!solo) {
       if (tid == 0) gran_store(rs, ((unsigned)(m % kSumSlots) * (unsigned)a.H + (unsigned)tile) * 16u, red32[m & 1], tag, plain);
-      if constexpr (COLS && CPL == 2) {
+#ifndef IRLMX_PAIR_BATCHED_PUBLISH
+#define IRLMX_PAIR_BATCHED_PUBLISH 0
+#endif
+      if constexpr (COLS && CPL == 2 && !IRLMX_PAIR_BATCHED_PUBLISH) {
         store_rows();
       } else if constexpr (COLS) {
         // column quads (width 256: 8 rows per thread): the staged rows, kPub per
