@@ -691,3 +691,50 @@ def test_grid_shape_cap_and_nonfinite(dev, monkeypatch):
         for x, y in zip(g_, r_):
             assert torch.equal(x.view(torch.int64) if x.dtype == torch.float64 else x,
                                y.view(torch.int64) if y.dtype == torch.float64 else y)
+
+
+@pytest.mark.gpu
+def test_deferred_convergence_caps_and_nan(dev, monkeypatch):
+    """The fused kernels test convergence once per 32-sweep block and replay the
+    block that holds the stopping sweep (run_deferred; VI and the widest rows: a
+    ballot per sweep, run_each).  Against the per-sweep shape, which reduces
+    every sweep: sweep counts, statuses and vectors bit for bit for iteration
+    caps on both sides of block boundaries (1, 31, 32, 33, 64, 65, 100), for the
+    uncapped runs, and for soft VI / VI stopped by a NaN (inf reward)."""
+    from irlmx import DeviceMDP, ops
+    sweep_env = {"IRLMX_FUSED_MAX_STATES": "0", "IRLMX_CLUSTER": "0"}
+    size, B = 7, 3
+    n = size * size
+    rng = np.random.default_rng(11)
+    mdp = DeviceMDP.icy_gridworld(size, np.array([0.1, 0.2, 0.3]), device=dev)
+    tm = ops.terminal_mask([n - 1], n, batch=B, device=dev)
+    r = torch.as_tensor(rng.uniform(0.0, 1.2, (B, n)), device=dev)
+    phi = torch.as_tensor(np.tile(O.terminal_reward([n - 1], n), (B, 1)), device=dev)
+    p0 = torch.zeros((B, n), dtype=torch.float64, device=dev)
+    p0[:, 0] = 1.0
+    r_nan = r.clone()
+    r_nan[1, 5] = float("inf")
+
+    def run(env, cap):
+        for k in sweep_env:
+            monkeypatch.delenv(k, raising=False)
+        for k, v in env.items():
+            monkeypatch.setenv(k, v)
+        assert (ops.execution_plan(mdp, "forward")["shape"] == "fused") == (not env)
+        pi = ops.backward_maxent(mdp, r, tm)
+        f = ops.forward_svf(mdp, p0, tm, pi, max_iter=cap)
+        s = ops.soft_backward(mdp, r, phi, 0.7, max_iter=cap)
+        v = ops.value_iteration(mdp, r, 0.9, max_iter=cap)
+        sn = ops.soft_backward(mdp, r_nan, phi, 0.7, max_iter=cap)
+        vn = ops.value_iteration(mdp, r_nan, 0.9, max_iter=cap)
+        return [f, s, v, sn, vn]
+
+    for cap in (1, 31, 32, 33, 64, 65, 100, 0):
+        a, b = run({}, cap), run(sweep_env, cap)
+        for what, x, y in zip(("forward", "soft", "vi", "soft_nan", "vi_nan"), a, b):
+            for i, (u, w) in enumerate(zip(x, y)):
+                if torch.is_tensor(u):
+                    assert u.shape == w.shape and torch.equal(torch.nan_to_num(u, nan=7.0), torch.nan_to_num(w, nan=7.0)), (cap, what, i)
+        if cap == 0:
+            assert int(a[3][3][1]) == 1 and int(a[4][2][1]) == 1  # IRLMX_NONFINITE for the inf-reward instance
+

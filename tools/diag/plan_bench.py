@@ -19,7 +19,7 @@ rng = np.random.default_rng(5)
 r = torch.as_tensor(rng.uniform(0, 1.5, (B, n)) if os.environ.get("RAND") else np.ones((B, n)), device=dev)
 p0 = torch.zeros((B, n), dtype=torch.float64, device=dev); p0[:, 0] = 1.0
 keys = ("IRLMX_NT", "IRLMX_PAIR", "IRLMX_CLUSTER_R", "IRLMX_CLUSTER_G", "IRLMX_STAMPS", "IRLMX_CLUSTER", "IRLMX_FUSED",
-        "IRLMX_DEFER")
+        "IRLMX_DEFER", "IRLMX_FWD_LAG", "IRLMX_EAGER_SUMMARY")
 pi = ops.backward_maxent(mdp, r, tm)
 torch.cuda.synchronize()
 ref = None
