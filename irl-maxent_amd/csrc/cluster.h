@@ -29,7 +29,7 @@ constexpr size_t kMaxLdsBytes = 160 * 1024;  // LDS per CU (one workgroup per CU
 // most kRescaleEvery apart), so between two such blocks a tile can run ahead
 // of a distant tile by up to kRescaleEvery blocks; its summary for block m + 4
 // must not land in the slot a slow tile is still polling for block m.
-constexpr int kSumSlots = 8;
+constexpr int kSumSlots = kRescaleEvery < 8 ? 8 : kRescaleEvery + 1;
 static_assert(kSumSlots > kRescaleEvery, "summary slots must outlast the rescale period");
 constexpr size_t kClusterStaticLds = 128;     // cluster_kernel's own __shared__ variables (resident flag, stamps)
 constexpr int kModeFwd = 0;
