@@ -720,7 +720,10 @@ __global__ void __launch_bounds__(NT) cluster_kernel(ClusterArgs a) {
         // thread at a time, all LDS reads in flight before the stores (the plain
         // loop waits out one LDS round trip per row): config 4 backward 302.6 ->
         // 293.6 ms; no gain for column pairs at width 128 (23.5 vs 23.7 ms)
-        constexpr int kPub = 4;
+#ifndef IRLMX_KPUB
+#define IRLMX_KPUB 4
+#endif
+        constexpr int kPub = IRLMX_KPUB;
         const int nA = pubA1 - own0, ntot = nA + (own1 - pubB0);
         for (int k0 = 0; k0 < ntot; k0 += kPub * NT) {
           int ls[kPub];
