@@ -1,7 +1,7 @@
 #!/usr/bin/env python
 """Summarise hipcc -Rpass-analysis=kernel-resource-usage remarks per kernel.
 
-usage: python tools/kernel_resources.py csrc/file.hip [more.hip ...]
+usage: python tools/kernel_resources.py [csrc/file.hip ...]   (default: every irl-maxent_amd/csrc/*.hip)
 """
 import re
 import subprocess
@@ -31,4 +31,7 @@ def main(files):
                   f"lds={r.get('LDS Size [bytes/block]','?')}")
 
 if __name__ == "__main__":
-    main(sys.argv[1:])
+    import glob
+    import os
+    here = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    main(sys.argv[1:] or sorted(glob.glob(os.path.join(here, "irl-maxent_amd", "csrc", "*.hip"))))
