@@ -373,8 +373,22 @@ __global__ void __launch_bounds__(NT) cluster_kernel(ClusterArgs a) {
     if constexpr (COLS) {
       const unsigned ob = slot_bits(own_bits);
       double dmax = 0.0;
+#ifndef IRLMX_FWD_BRANCH_ACCOUNT
+#define IRLMX_FWD_BRANCH_ACCOUNT 0
+#endif
+      // (IRLMX_FWD_BRANCH_ACCOUNT with wave-uniform slot predicates: a scalar
+      // branch per slot around the owned-delta update instead of computing it
+      // for every slot and selecting -- the empty asm keeps the compiler from
+      // speculating the body back into selects)
       auto account = [&](int j, double nv, double self) {
-        if (MODE == kModeFwd && ((ob >> j) & 1u)) dmax = fmax(dmax, fabs(nv - self));
+        if constexpr (MODE == kModeFwd && kUniformSlots && IRLMX_FWD_BRANCH_ACCOUNT) {
+          if ((ob >> j) & 1u) {
+            asm volatile("");
+            dmax = fmax(dmax, fabs(nv - self));
+          }
+        } else if (MODE == kModeFwd && ((ob >> j) & 1u)) {
+          dmax = fmax(dmax, fabs(nv - self));
+        }
       };
       if constexpr (kSplitEdges) {  // band edge rows (old values) out: column 0 / column 1 arrays
         double* t = edge_row(i & 1, bb + 1, 0);
