@@ -48,7 +48,7 @@ struct ClusterArgs {
   const double* vin;       // forward: p0 [B][S]; backward: reward [B][S]
   const uint8_t* term;     // backward: terminal mask [B][S]
   const int32_t* bad;      // forward: non-finite policy flags [B]
-  const unsigned long long* growth;  // backward: per-instance growth bound bits [B]
+  const unsigned long long* growth;  // backward: per-instance growth / decay bound bits [2][B]
   double eps;
   long long max_iter;
   long long n_sweeps;      // backward: collapsed sweeps (2S - 1)
@@ -230,6 +230,6 @@ constexpr int kClusterNotResident = 2;
 
 bool cluster_plan(int W, int H, int B, int mode, ClusterPlan* out);
 int cluster_run(int mode, const ClusterPlan& p, ClusterArgs a, int B, hipStream_t st);
-__global__ void bwd_growth_kernel(const double* __restrict__ bw, int S, unsigned long long* __restrict__ growth);
+__global__ void bwd_growth_kernel(const double* __restrict__ bw, int S, int B, unsigned long long* __restrict__ growth);
 
 }  // namespace irlmx

@@ -262,17 +262,23 @@ __global__ void __launch_bounds__(NT) cluster_kernel(ClusterArgs a) {
 
   int T = a.T;
   // Backward rescaling period: blocks between rescales (see the block loop).
-  // Growth over P_max blocks stays below 2^900 (g^(P_max T) < 2^900).
+  // Between two rescales the partition vector neither grows nor shrinks by more
+  // than 2^900: its maximum grows at most by g = max_s sum_k w_k(s) per sweep
+  // and shrinks at most by d = the smallest positive weight (every grid state is
+  // some in-grid neighbour's stencil target with a positive weight, so the state
+  // holding the maximum feeds at least d times it into the next sweep).  The
+  // sweeps between rescales, T * p_max, are capped at 900 / log2 of either rate
+  // -- which shortens the solo backward's 256-sweep blocks (kSoloBwdT) where
+  // the rewards are very negative (decay) or the growth is near 2 per sweep.
   int p_max = 1;
   if (MODE == kModeBwd) {
-    // cap the block so the growth over T sweeps stays below 2^900
     const double g = bits_double(a.growth[inst]);
+    const double d = bits_double(a.growth[a.btot + inst]);
     if (a.rescale && isfinite(g)) {
       int cap = 1 << 20;
-      if (g > 2.0) {
-        cap = (int)floor(900.0 / log2(g)) - 1;
-        T = max(1, min(T, cap));
-      }
+      if (g > 1.0) cap = max(1, (int)floor(900.0 / log2(g)) - 1);
+      if (d > 0.0 && d < 1.0) cap = min(cap, max(1, (int)floor(900.0 / -log2(d)) - 1));
+      T = max(1, min(T, cap));
       p_max = max(1, min(kRescaleEvery, cap / T));
     }
   }
@@ -914,24 +920,32 @@ __global__ void __launch_bounds__(NT) cluster_kernel(ClusterArgs a) {
 
 namespace irlmx {
 
-// Per-instance bound on the backward's per-sweep growth: max_s sum_k bw[b][k][s]
-// (reward-folded weights, fixed_point.hip bwd_weights_kernel).
-__global__ void bwd_growth_kernel(const double* __restrict__ bw, int S, unsigned long long* __restrict__ growth) {
+// Per-instance bounds on the backward's per-sweep growth and decay (reward-folded
+// weights, fixed_point.hip bwd_weights_kernel): growth[b] = max_s sum_k bw[b][k][s],
+// growth[B + b] = the smallest positive weight (both as float64 bits; the
+// weights are non-negative, so the bits order like the values).
+__global__ void bwd_growth_kernel(const double* __restrict__ bw, int S, int B, unsigned long long* __restrict__ growth) {
   const int b = blockIdx.x;
   const double* wb = bw + (size_t)b * kStencilK * S;
-  unsigned long long mx = 0ull;
+  unsigned long long mx = 0ull, mn = ~0ull;
   for (int s = threadIdx.x; s < S; s += blockDim.x) {
     double row = 0.0;
-    for (int k = 0; k < kStencilK; ++k) row += wb[(size_t)k * S + s];
+    for (int k = 0; k < kStencilK; ++k) {
+      const double x = wb[(size_t)k * S + s];
+      row += x;
+      if (x > 0.0) mn = min(mn, abs_bits(x));
+    }
     mx = max(mx, abs_bits(row));
   }
-  __shared__ unsigned long long red[16];
+  __shared__ unsigned long long red[2][16];
   mx = wave_max_u64(mx);
-  if ((threadIdx.x & 63) == 0) red[threadIdx.x / 64] = mx;
+  mn = ~wave_max_u64(~mn);
+  if ((threadIdx.x & 63) == 0) { red[0][threadIdx.x / 64] = mx; red[1][threadIdx.x / 64] = mn; }
   __syncthreads();
   if (threadIdx.x == 0) {
-    for (int i = 1; i < (int)(blockDim.x / 64); ++i) mx = max(mx, red[i]);
+    for (int i = 1; i < (int)(blockDim.x / 64); ++i) { mx = max(mx, red[0][i]); mn = min(mn, red[1][i]); }
     growth[b] = mx;
+    growth[B + b] = mn == ~0ull ? 0ull : mn;  // no positive weight: no decay bound (0)
   }
 }
 

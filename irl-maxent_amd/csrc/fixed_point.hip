@@ -129,7 +129,7 @@ struct Ws {
   // cluster shape (stencil layouts too large for one CU)
   unsigned long long* gran;   // [B][2][S] x 16 B
   unsigned long long* sgran;  // [B][3][H] x 16 B
-  unsigned long long* growth; // [B]
+  unsigned long long* growth; // [2][B] growth / decay bounds
   int* err;                   // [1]
   size_t total;
 };
@@ -182,7 +182,7 @@ static Ws carve(const Model& m, int op, void* base) {
   w.gran = (unsigned long long*)take(cl || dg ? 2 * B * S * 16 : (gr ? 3 * B * S * 16 : 0));
   w.sgran = (unsigned long long*)take(cl ? (kSumSlots + 1) * B * (size_t)m.H * 16
                                          : (gr ? 4 * B * (size_t)gp.bpi * 16 : (dg ? B * (size_t)dp.bpi * 16 : 0)));
-  w.growth = (unsigned long long*)take(cl ? B * sizeof(unsigned long long) : 0);
+  w.growth = (unsigned long long*)take(cl ? 2 * B * sizeof(unsigned long long) : 0);
   w.err = (int*)take(cl || gr || dg ? 4 * sizeof(int) : 0);
   w.total = off;
   return w;
@@ -2703,7 +2703,7 @@ extern "C" int irlmx_backward_maxent(const irlmx_mdp* mdp, const double* reward,
   // (without rescaling the partition vector overflows like the reference's: such
   // calls take the per-sweep shape, whose non-finite bookkeeping is per sweep)
   if (m.stencil && m.A <= kMaxActions && rescale && cluster_plan(m.W, m.H, m.B, kModeBwd, &cp)) {
-    hipLaunchKernelGGL(bwd_growth_kernel, dim3(m.B), dim3(1024), 0, st, ws.wgt, m.S, ws.growth);
+    hipLaunchKernelGGL(bwd_growth_kernel, dim3(m.B), dim3(1024), 0, st, ws.wgt, m.S, m.B, ws.growth);
     ClusterArgs ca{};
     ca.W = m.W; ca.H = m.H; ca.S = m.S; ca.A = m.A;
     ca.tab_shared = m.shared ? 1 : 0;

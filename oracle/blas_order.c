@@ -36,16 +36,18 @@
 
 #define NBMAX 2048
 
-/* y[s] = sum_t M[s][t] x[t], M row-major n x n, in OpenBLAS Haswell dgemv_t order. */
-int blas_order_dgemv_rows(const double* M, int n, const double* x, double* y) {
-  if (n <= 0 || (n & 3) > 1) return -1;
+/* y[s] = sum_t M[s][t] x[t], M row-major n x n, in OpenBLAS Haswell dgemv_t order
+ * with column blocks of nbmax (the tests run it with an unbounded block too, to
+ * show that numpy's results at S > 2048 do depend on the NBMAX split). */
+int blas_order_dgemv_rows_nb(const double* M, int n, const double* x, double* y, int nbmax) {
+  if (n <= 0 || (n & 3) > 1 || nbmax <= 0) return -1;
   const int m1 = n - (n & 3), n4 = n & ~3;
   for (int s = 0; s < n; ++s) {
     const double* a = M + (size_t)s * n;
     const int fused = s < n4;
     double out = 0.0;
-    for (int lo = 0; lo < m1; lo += NBMAX) {
-      const int hi = lo + NBMAX < m1 ? lo + NBMAX : m1;
+    for (int lo = 0; lo < m1; lo += nbmax) {
+      const int hi = nbmax < m1 - lo ? lo + nbmax : m1;
       double l[4] = {0.0, 0.0, 0.0, 0.0};
       for (int t = lo; t < hi; ++t) {
         const int q = (t - lo) & 3;
@@ -57,6 +59,10 @@ int blas_order_dgemv_rows(const double* M, int n, const double* x, double* y) {
     y[s] = out;
   }
   return 0;
+}
+
+int blas_order_dgemv_rows(const double* M, int n, const double* x, double* y) {
+  return blas_order_dgemv_rows_nb(M, n, x, y, NBMAX);
 }
 
 /*
@@ -217,4 +223,72 @@ long long blas_order_forward_svf(const double* P, int S, int A, const double* p0
   }
   free(pa); free(x); free(y); free(dn);
   return it;
+}
+
+/*
+ * The same dgemv_t order over a sparse matrix (CSR, ascending columns per row):
+ * numpy's dense dot products with the zero entries skipped.  A skipped entry
+ * contributes fma(0, x, acc) = acc (or acc + 0 * x = acc) exactly while x is
+ * finite -- the lane accumulators start at +0 and never become -0 -- so the
+ * result equals blas_order_dgemv_rows on the dense matrix bit for bit
+ * (tests/test_oracle_blas_order.py pins it), at O(nnz) instead of O(S^2): the
+ * restatement then reaches 64x64 grids (S = 4096, the two NBMAX blocks).
+ */
+int blas_order_dgemv_rows_csr(const int64_t* indptr, const int32_t* indices, const double* data, int n,
+                              const double* x, double* y) {
+  if (n <= 0 || (n & 3) > 1) return -1;
+  const int m1 = n - (n & 3), n4 = n & ~3;
+  for (int s = 0; s < n; ++s) {
+    const int fused = s < n4;
+    int64_t e = indptr[s];
+    const int64_t e1 = indptr[s + 1];
+    double out = 0.0;
+    for (int lo = 0; lo < m1; lo += NBMAX) {
+      const int hi = lo + NBMAX < m1 ? lo + NBMAX : m1;
+      double l[4] = {0.0, 0.0, 0.0, 0.0};
+      for (; e < e1 && indices[e] < hi; ++e) {
+        const int t = indices[e];
+        const int q = (t - lo) & 3;
+        l[q] = fused ? fma(data[e], x[t], l[q]) : l[q] + data[e] * x[t];
+      }
+      out = out + ((l[0] + l[2]) + (l[1] + l[3]));
+    }
+    for (; e < e1; ++e) out = fma(data[e], x[indices[e]], out);
+    y[s] = out;
+  }
+  return 0;
+}
+
+/*
+ * local_action_probabilities (maxent.py:119-159) in numpy's order on per-action
+ * CSR matrices P_a[s, t] (the slices p[a] of maxent.py:143), stacked as one CSR
+ * of A * S rows: the statements of blas_order_backward_maxent with
+ * blas_order_dgemv_rows_csr for the dot products.
+ */
+int blas_order_backward_maxent_csr(const int64_t* indptr, const int32_t* indices, const double* data, int S, int A,
+                                   const uint8_t* term, const double* er, double* pi) {
+  if (S <= 0 || A <= 0 || (S & 3) > 1) return -1;
+  double* zs = malloc((size_t)S * sizeof(double));
+  double* dot = malloc((size_t)S * sizeof(double));
+  double* za = malloc((size_t)S * A * sizeof(double));
+  if (!zs || !dot || !za) {
+    free(zs); free(dot); free(za);
+    return -2;
+  }
+  for (int s = 0; s < S; ++s) zs[s] = term[s] ? 1.0 : 0.0;
+  for (int it = 0; it < 2 * S; ++it) {
+    for (int a = 0; a < A; ++a) {
+      blas_order_dgemv_rows_csr(indptr + (size_t)a * S, indices, data, S, zs, dot);
+      for (int s = 0; s < S; ++s) za[(size_t)s * A + a] = er[s] * dot[s];
+    }
+    for (int s = 0; s < S; ++s) {
+      double z = za[(size_t)s * A];
+      for (int a = 1; a < A; ++a) z = z + za[(size_t)s * A + a];
+      zs[s] = z;
+    }
+  }
+  for (int s = 0; s < S; ++s)
+    for (int a = 0; a < A; ++a) pi[(size_t)s * A + a] = za[(size_t)s * A + a] / zs[s];
+  free(zs); free(dot); free(za);
+  return 0;
 }

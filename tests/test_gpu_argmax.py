@@ -351,3 +351,26 @@ def test_backward_numpy_order_cached_against_restatement(dev, size):
     mdp = DeviceMDP.icy_gridworld(size, 0.2, device=dev)
     pi = ops.backward_maxent_numpy_order(mdp, np.exp(r), ops.terminal_mask([n - 1], n, device=dev))
     assert np.array_equal(pi[0].cpu().numpy(), ref)
+
+
+def test_backward_numpy_order_64x64_against_restatement(dev):
+    """64x64 (S = 4096, the largest model the drop-ins run in numpy's order):
+    the device's numpy-order backward against the C restatement of numpy's
+    order (its sparse form, oracle/blas_order.c, pinned to the dense form and to
+    np.dot at S = 4096 -- both NBMAX = 2048 column blocks -- in
+    tests/test_oracle_blas_order.py), rewards near -ln 4 so that the 2 S = 8192
+    sweeps stay finite: bit for bit, through ops on the device-built table and
+    through the drop-in on the uploaded dense table."""
+    import maxent as M
+    from irlmx import DeviceMDP, ops
+    size = 64
+    n = size * size
+    r = -np.log(4.0) + np.random.default_rng(64).uniform(-0.05, 0.05, n)
+    ref = O.backward_maxent_blas_order_csr(O.icy_gridworld_csr(size, 0.2), [n - 1], r)
+    assert np.isfinite(ref).all()
+    mdp = DeviceMDP.icy_gridworld(size, 0.2, device=dev)
+    pi = ops.backward_maxent_numpy_order(mdp, np.exp(r), ops.terminal_mask([n - 1], n, device=dev))
+    assert np.array_equal(pi[0].cpu().numpy(), ref), np.max(np.abs(pi[0].cpu().numpy() - ref))
+    got = M.local_action_probabilities(O.icy_gridworld_table(size, 0.2), [n - 1], r)
+    assert np.array_equal(got, ref)
+    assert np.array_equal(np.argmax(got, axis=1), np.argmax(ref, axis=1))

@@ -308,7 +308,7 @@ def test_causal_128_config5(dev):
     """Config 5: MaxCausalEnt soft VI on 128x128, fp64, discount
     0.7, theta ~ U(0, 1.5) (seed 5), against the reference's own output at that size
     (tests/golden/causal_128.npz, tools/gen_golden.py --heavy): identical sweep count,
-    max|d pi| <= 1e-9 * max|pi_ref|; then the causal forward pass runs to
+    max|d pi| <= 1e-9 * max|pi_ref|, argmax identical at every state; then the causal forward pass runs to
     convergence on the device policy (sweep count and SVF against the oracle's
     converged fixture)."""
     from irlmx import DeviceMDP, ops
@@ -321,6 +321,12 @@ def test_causal_128_config5(dev):
     got = pi[0].cpu().numpy()
     ref = z["pi"]
     assert np.max(np.abs(got - ref)) <= 1e-9 * np.max(np.abs(ref)), np.max(np.abs(got - ref))
+    # argmax (maxent.py:341 policy indices) bit-exact against the reference's own
+    # policy: the only exact tie (state 0, the corner whose two wall actions have
+    # identical rows) falls to the first index on both sides; the nearest other
+    # top-two gap is 4.4e-5 relative, far above the 1e-9 agreement
+    ga, ra = np.argmax(got, axis=1), np.argmax(ref, axis=1)
+    assert np.array_equal(ga, ra), np.flatnonzero(ga != ra)[:8]
     p0 = np.zeros(n)
     p0[0] = 1.0
     # forward to convergence on the device's own policy, against the oracle's
@@ -566,6 +572,85 @@ def test_cluster_stops_at_block_edges(dev, monkeypatch):
             assert out["cluster"][1].tolist() == [cap] * B
     for k in keys:
         monkeypatch.delenv(k, raising=False)
+
+
+def test_cluster_stops_ghosts_wider_than_tiles(dev, monkeypatch):
+    """Config 2's forward plan shape R = 8 owned rows < G = 12 ghost rows (C = 8
+    tiles per 64x64 instance, ghost rows from tiles two away; T = 12 sweeps per
+    block): a cap at every sweep of the first three blocks and around later
+    block edges, and the natural stops at two eps -- SVFs, sweep counts and
+    statuses bit-identical to the per-sweep shape ("Stop
+    protocol", states why every tile sees the stopping sweep)."""
+    from irlmx import DeviceMDP, ops
+    size, B = 64, 2
+    n = size * size
+    mdp = DeviceMDP.icy_gridworld(size, [0.2, 0.3], device=dev)
+    tm = ops.terminal_mask([n - 1], n, batch=B, device=dev)
+    p0 = np.zeros((B, n))
+    p0[np.arange(B), [0, 1500]] = 1.0
+    keys = ("IRLMX_FUSED_MAX_STATES", "IRLMX_CLUSTER", "IRLMX_CLUSTER_R", "IRLMX_CLUSTER_G")
+    for k in keys:
+        monkeypatch.delenv(k, raising=False)
+    pi = ops.backward_maxent(mdp, np.ones((B, n)), tm)
+    shapes = (("sweep", {"IRLMX_FUSED_MAX_STATES": "0", "IRLMX_CLUSTER": "0"}),
+              ("cluster", {"IRLMX_FUSED_MAX_STATES": "0", "IRLMX_CLUSTER_R": "8", "IRLMX_CLUSTER_G": "12"}))
+    for k, v in shapes[1][1].items():
+        monkeypatch.setenv(k, v)
+    plan = ops.execution_plan(mdp, "forward")
+    assert (plan["shape"], plan["R"], plan["G"], plan["C"]) == ("cluster", 8, 12, 8), plan
+    runs = [(1e-5, c) for c in list(range(1, 38)) + [59, 60, 61, 143, 144, 145, 1199, 1200, 1201]]
+    runs += [(2e-3, 0), (1e-5, 0)]
+    for eps, cap in runs:
+        out = {}
+        for name, env in shapes:
+            for k in keys:
+                monkeypatch.delenv(k, raising=False)
+            for k, v in env.items():
+                monkeypatch.setenv(k, v)
+            out[name] = ops.forward_svf(mdp, p0, tm, pi, eps=eps, max_iter=cap)
+        for i, what in enumerate(("svf", "sweeps", "status")):
+            assert torch.equal(out["sweep"][i], out["cluster"][i]), (eps, cap, what)
+        if cap:
+            assert out["cluster"][1].tolist() == [cap] * B
+    for k in keys:
+        monkeypatch.delenv(k, raising=False)
+
+
+def test_solo_backward_rescale_extremes(dev, monkeypatch):
+    """One 64x64 instance on one tile (config 2's backward: blocks of up to
+    kSoloBwdT = 256 sweeps between rescales) at uniform rewards where the
+    partition vector grows by ~2 per sweep (-0.7, ln 0.5, 0) or decays by ~40 per
+    sweep (-5; 256 unscaled sweeps would underflow to 0, a NaN policy): finite,
+    bit-identical to 16-sweep blocks and to the per-sweep shape (power-of-two
+    rescaling is exact), within 1e-9 of the CSR oracle."""
+    from irlmx import DeviceMDP, ops
+    size = 64
+    n = size * size
+    mdp = DeviceMDP.icy_gridworld(size, 0.2, device=dev)
+    tm = ops.terminal_mask([n - 1], n, device=dev)
+    mats = O.icy_gridworld_csr(size, 0.2)
+    keys = ("IRLMX_FUSED_MAX_STATES", "IRLMX_CLUSTER", "IRLMX_SOLO_T")
+    for rv in (-0.7, float(np.log(0.5)), 0.0, -5.0):
+        r = np.full(n, rv)
+        out = {}
+        for name, env in (("solo", {"IRLMX_FUSED_MAX_STATES": "0"}),
+                          ("solo16", {"IRLMX_FUSED_MAX_STATES": "0", "IRLMX_SOLO_T": "16"}),
+                          ("sweep", {"IRLMX_FUSED_MAX_STATES": "0", "IRLMX_CLUSTER": "0"})):
+            for k in keys:
+                monkeypatch.delenv(k, raising=False)
+            for k, v in env.items():
+                monkeypatch.setenv(k, v)
+            if name == "solo":
+                plan = ops.execution_plan(mdp, "backward")
+                assert plan["C"] == 1 and plan["shape"] == "cluster", plan
+            out[name] = ops.backward_maxent(mdp, r, tm)[0]
+        for k in keys:
+            monkeypatch.delenv(k, raising=False)
+        assert bool(torch.isfinite(out["solo"]).all()), rv
+        assert torch.equal(out["solo"], out["solo16"]) and torch.equal(out["solo"], out["sweep"]), rv
+        ref = O.backward_maxent_csr(mats, [n - 1], r)
+        got = out["solo"].cpu().numpy()
+        assert np.max(np.abs(got - ref)) <= 1e-9 * np.max(np.abs(ref)), rv
 
 
 def test_width256_quads_bit_identical(dev, monkeypatch):

@@ -22,6 +22,12 @@ irlmx.demos.sample with seed 1234 + b):
                the first 2 irl_causal steps (maxent.py:437-450) of the bench's
                c5 workload (one instance, discount 0.7).
 
+  run_c3.npz   128x128, B = 64: instances b = 0 and 63 run to the reference's own
+               stopping rule (maxent.py:236-255, eps = 1e-4) -- step count,
+               per-step forward sweeps and theta summaries, theta after steps
+               6, 15 and 25 (the bench's timed window at W = 5, K = 20) and
+               the final reward (theta, F = I).  ~2.5 h per instance.
+
   dense2048.npz  a seeded random dense MDP (S = 2048, A = 4, every entry
                nonzero; oracle random_dense_mdp() regenerates it bit for bit on any
                host), run through the dense oracle (the reference's own numpy
@@ -29,7 +35,8 @@ irlmx.demos.sample with seed 1234 + b):
                backward, forward, soft VI + causal forward, VI and its
                action-average form, with sweep counts.
 
-Usage: python tools/gen_full_fixtures.py [c3 c4 c5 dense]   (~25 min on 8 cores)
+Usage: python tools/gen_full_fixtures.py [c3 c4 c5 dense c3run]
+       (~25 min on 8 cores without c3run)
 """
 
 import os
@@ -99,6 +106,29 @@ def job_irl(args):
     return cfg, b, out
 
 
+RUN_KEEP = (1, 2, 3, 6, 15, 25)
+
+
+def job_run(args):
+    """Whole irl run of one bench instance (run_c3.npz)."""
+    cfg, size, n_total, b = args
+    t0 = time.time()
+    n = size * size
+    slip, mats, e_f, p0 = bench_instance(size, b, n_total)
+
+    def progress(k, theta, k_f, delta):
+        if k <= 3 or k % 25 == 0:
+            print(f"[run {cfg} b={b}] step {k} k_f={k_f} delta={delta:.3e} {time.time() - t0:.0f}s", flush=True)
+
+    res = O.irl_run_csr(mats, e_f, p0, [n - 1], keep_steps=RUN_KEEP, on_step=progress)
+    out = {"slip": np.array(slip), "steps": np.array(res["steps"]), "k_f": np.array(res["k_f"]),
+           "delta": np.array(res["delta"]), "theta_sum": np.array(res["theta_sum"]), "theta": res["theta"]}
+    for k, th in res["theta_at"].items():
+        out[f"theta_at{k}"] = th
+    print(f"[run {cfg} b={b}] steps={res['steps']} {time.time() - t0:.0f}s", flush=True)
+    return "run_" + cfg, b, out
+
+
 def job_dense(_):
     t0 = time.time()
     os.environ["OPENBLAS_NUM_THREADS"] = "4"
@@ -137,6 +167,8 @@ def main():
         jobs += [(job_irl, ("c3", 128, 64, b, 3, False)) for b in (0, 63)]
     if "c4" in which:
         jobs += [(job_irl, ("c4", 256, 32, b, 2, False)) for b in (0, 31)]
+    if "c3run" in which:
+        jobs += [(job_run, ("c3", 128, 64, b)) for b in (0, 63)]
     if "c5" in which:
         jobs += [(job_c5_forward, None), (job_irl, ("c5", 128, 1, 0, 2, True))]
     with Pool(len(jobs)) as pool:
@@ -153,6 +185,12 @@ def main():
         for k, v in out.items():
             d[f"{key}__{k}" if key != "fwd" else f"fwd__{k}"] = v
     for cfg, d in files.items():
+        if cfg.startswith("run_"):
+            d["instances"] = np.array(sorted({int(k.split("__")[0]) for k in d}))
+            path = os.path.join(OUT, f"{cfg}.npz")
+            np.savez_compressed(path, **d)
+            print("wrote", path, os.path.getsize(path), "bytes")
+            continue
         d["instances"] = np.array(sorted({int(k.split("__")[0]) for k in d if k.split("__")[0].isdigit()}))
         path = os.path.join(OUT, f"full_{cfg}.npz")
         np.savez_compressed(path, **d)
