@@ -106,6 +106,19 @@ def _latest(pattern):
     return files[-1] if files else None
 
 
+def _latest_profile(config):
+    """The newest profiles/r*_summary.json recorded for this workload config
+    (tools/parse_rocprof.py writes the config into it; c3 when absent)."""
+    import glob
+    for path in sorted(glob.glob(os.path.join(ROOT, "profiles", "r*_summary.json")), reverse=True):
+        try:
+            if json.load(open(path)).get("config", "c3") == config:
+                return path
+        except (OSError, ValueError):
+            continue
+    return None
+
+
 CPU_DENSE_MAX = 128   # larger dense fp64 tables do not fit host RAM (256x256: 137 GB); extrapolate
 
 
@@ -494,6 +507,8 @@ def main(argv=None):
     from irlmx.batch import BatchedMaxEnt
 
     size, per_gpu, desc, causal = CONFIGS[args.config]
+    if (args.size and args.size != size) or (args.batch and args.batch != per_gpu):
+        desc += f" [overridden: {args.size or size}x{args.size or size}, {args.batch or per_gpu} instances per GPU]"
     size = args.size or size
     per_gpu = args.batch or per_gpu
     S = size * size
@@ -602,7 +617,7 @@ def main(argv=None):
             # the state and weights stay on chip across sweeps, HBM carries the halo exchanges
             "algorithmic_bytes_per_launch": kd["bytes"] / kd["launches"],
         }
-        ppath = args.profile or _latest("r*_summary.json")
+        ppath = args.profile or _latest_profile(args.config)
         default_cfg = not args.size and not args.batch
         if ppath and os.path.exists(ppath) and default_cfg:
             prof = json.load(open(ppath))

@@ -17,18 +17,24 @@ constexpr int kSptMaxQuadFwd = 12;  // forward with column quads (register budge
 // VGPRs spill to scratch, yet 3.8 % faster at config 4 than 12: G = 8 ghost
 // rows instead of 4 halve the exchanges)
 constexpr int kSptMaxQuadBwd = 16;
+// backward with column quads and compact weights (layout 4, width 256): three
+// weights per state instead of five, so 20 states per lane fit the registers
+constexpr int kSptMaxQuadBwdCW = 20;
 constexpr int kTMax = 16;          // max sweeps per block (= max ghost rows)
 constexpr int kSoloBwdT = 256;     // backward sweeps per block of a solo tile (no ghost rows)
 #ifndef IRLMX_RESCALE_EVERY
-#define IRLMX_RESCALE_EVERY 4
+#define IRLMX_RESCALE_EVERY 16
 #endif
 constexpr int kRescaleEvery = IRLMX_RESCALE_EVERY;  // backward: max blocks between rescales
 constexpr size_t kMaxLdsBytes = 160 * 1024;  // LDS per CU (one workgroup per CU)
 // Tile-summary granule slots per instance, indexed by block % kSumSlots.  A
 // backward tile reads the other tiles' summaries only on rescale blocks (at
 // most kRescaleEvery apart), so between two such blocks a tile can run ahead
-// of a distant tile by up to kRescaleEvery blocks; its summary for block m + 4
-// must not land in the slot a slow tile is still polling for block m.
+// of a distant tile by up to kRescaleEvery blocks; its summary for block
+// m + kRescaleEvery must not land in the slot a slow tile is still polling for
+// block m.  (The period is also capped per instance so that the partition
+// vector neither grows nor shrinks by more than 2^900 between two rescales:
+// cluster.hip, p_max.)
 constexpr int kSumSlots = kRescaleEvery < 8 ? 8 : kRescaleEvery + 1;
 static_assert(kSumSlots > kRescaleEvery, "summary slots must outlast the rescale period");
 constexpr size_t kClusterStaticLds = 128;     // cluster_kernel's own __shared__ variables (resident flag, stamps)
@@ -53,7 +59,7 @@ struct ClusterArgs {
   long long max_iter;
   long long n_sweeps;      // backward: collapsed sweeps (2S - 1)
   int rescale;
-  unsigned long long* gran;   // [B][2][S] x 16-byte tagged granule pairs (halo rows)
+  unsigned long long* gran;   // [B][gran_inst_len] x 16-byte tagged granule pairs (halo rows, see kGranRowPad)
   unsigned long long* sgran;  // [B][kSumSlots + 1][H] x 16-byte tagged granule pairs (tile summaries, XCC ids)
   int xcd_group;           // number the tiles of an instance within one XCD group
   unsigned salt;           // per-launch granule tag salt
@@ -71,7 +77,8 @@ struct ClusterArgs {
 struct ClusterPlan {
   int R, G, C, T, per_launch, spt, emax;
   size_t lds;
-  int pair;             // in-tile layout: 0 per state, 1 pair rows, 2 column pairs, 3 column quads
+  int pair;             // in-tile layout: 0 per state, 1 pair rows, 2 column pairs, 3 column quads,
+                        // 4 column quads with compact weights (backward, width 256)
   int nt;               // threads per workgroup
 };
 
@@ -87,6 +94,19 @@ typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
 #define IRLMX_POLL_SLEEP 1   // s_sleep units (64 cycles) between polling passes
 #endif
 constexpr int kGatherPerThread = 4;
+
+// Halo granule layout per instance: [2 parities][H rows][W + kGranRowPad] x 16 B,
+// parities and instances separated by a few more 128-B lines.  With the plain
+// [2][S] layout every tile's publication rows sat at power-of-two strides (rows
+// 4 KiB, tiles 64-128 KiB, parities and instances 256 KiB - 2 MiB apart), so
+// the publications of all tiles, both parities and all instances of an XCD
+// fell into the same few L2 sets: config 4 (width 256) wrote 274 GB of evicted
+// granule lines to HBM per backward launch, every store it made.  One extra
+// line per row and odd line offsets between parities and instances spread them
+// over the sets.
+constexpr int kGranRowPad = 8;                                    // granules (one 128-B line) per row
+__host__ __device__ inline size_t gran_par_len(int W, int H) { return (size_t)H * (W + kGranRowPad) + 24; }
+__host__ __device__ inline size_t gran_inst_len(int W, int H) { return 2 * gran_par_len(W, H) + 40; }
 
 // A granule buffer: its descriptor (and, in IRLMX_DEVICE_CHECKS builds, its
 // byte length for the offset checks).
@@ -228,8 +248,11 @@ constexpr int kClusterNonFinite = 1;
 // (coresident()): the call must be rerun on a shape without hand-offs
 constexpr int kClusterNotResident = 2;
 
-bool cluster_plan(int W, int H, int B, int mode, ClusterPlan* out);
+// compact: the backward's weights have the structure layout 4 needs
+// (bwd_compact_ok_kernel); the planner then considers it at width 256
+bool cluster_plan(int W, int H, int B, int mode, ClusterPlan* out, bool compact = false);
 int cluster_run(int mode, const ClusterPlan& p, ClusterArgs a, int B, hipStream_t st);
 __global__ void bwd_growth_kernel(const double* __restrict__ bw, int S, int B, unsigned long long* __restrict__ growth);
+__global__ void bwd_compact_ok_kernel(const double* __restrict__ row_val, int W, int H, int A, int* __restrict__ bad);
 
 }  // namespace irlmx

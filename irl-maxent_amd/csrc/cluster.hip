@@ -93,13 +93,37 @@ __device__ inline double dpp_shift_f64(double x) {
 //
 // LAY == 3 is the same with four columns per lane (CPL = 4): half the DPP
 // moves per state, and at width 256 one band row is one wave.
+//
+// LAY == 4 (backward, width 256): column quads with compact weights.  For the
+// gridworld tables the collapsed coefficients sum_a P[s, n, a] of the +x and
+// -x neighbours are equal wherever both are in the grid, the self coefficient
+// is 0 off the grid border, and an off-grid neighbour's coefficient is 0
+// (checked per call on the table: bwd_compact_ok_kernel).  A state then keeps
+// three weights in registers -- w_x for both horizontal neighbours, w_+y, w_-y
+// -- instead of five:
+//   * an off-grid horizontal neighbour reads 0 (the DPP shift's zero fill at
+//     lanes 0 and 63, where one band row is one wave), so fma(w_x, 0, acc) ==
+//     acc == fma(0, garbage, acc) of the five-weight chain;
+//   * the self term fma(w_0, v, 0) (+0 off the border): columns 0 and CPL - 1
+//     take w_0 from two per-row registers that hold it only in lane 0 / HW - 1
+//     (x = 0 / W - 1) and on the border rows y = 0 / H - 1, else 0; the middle
+//     columns from one 16-byte LDS entry per row that is 0 except on a border
+//     row.  No branch: the sweep stays one straight-line block (a per-row
+//     branch measured 2.3x slower, the FMA chains of different rows no longer
+//     interleaving).
+// The FMA chain is the five-weight one, operand for operand, so the results
+// are bit-identical, with three weight registers per state instead of five.
+// The LDS band-edge array aliases the tile buffer, which the backward touches
+// only between blocks.
 template <int MODE, int SPT, int WT, int LAY, int NT>
 __global__ void __launch_bounds__(NT) cluster_kernel(ClusterArgs a) {
   constexpr bool PAIR = LAY >= 1, COLS = LAY >= 2;
-  constexpr int CPL = LAY == 3 ? 4 : 2;                  // COLS: columns per lane
+  constexpr bool CW = LAY == 4;                          // compact weights (see above)
+  constexpr int CPL = LAY >= 3 ? 4 : 2;                  // COLS: columns per lane
   static_assert(LAY != 1 || (SPT % 2 == 0 && (WT == 64 || WT == 128)), "pair rows: even SPT, width 64/128");
   static_assert(LAY != 2 || (SPT % 2 == 0 && (WT == 64 || WT == 128)), "column pairs: even SPT, width 64/128");
   static_assert(LAY != 3 || (SPT % 4 == 0 && (WT == 128 || WT == 256)), "column quads: SPT % 4, width 128/256");
+  static_assert(LAY != 4 || (MODE == kModeBwd && SPT % 4 == 0 && WT == 256), "compact weights: backward, width 256");
   constexpr int RW = COLS ? SPT / CPL : 1;               // COLS: rows per band
   constexpr int HW = COLS ? WT / CPL : 1;                // COLS: lanes per band
   constexpr int NB = COLS ? NT / HW : 1;                 // COLS: bands
@@ -169,10 +193,16 @@ __global__ void __launch_bounds__(NT) cluster_kernel(ClusterArgs a) {
   // COLS keeps a single tile buffer (ghost staging, the backward's final sweep)
   double* bufB = bufA + (COLS ? 0 : blen);
   double* snap = bufB + blen;                                            // forward: block-start state
-  // COLS: band edge rows [2 parities][NB + 2 (zero band at both ends)][2: top, bottom][HW][QW] double2
-  double2* bnd = (double2*)(snap + (MODE == kModeFwd ? a.emax : 0));
+  // COLS: band edge rows [2 parities][NB + 2 (zero band at both ends)][2: top, bottom][HW][QW] double2;
+  // CW: aliasing the tile buffer (used only inside a block's sweeps; the tile
+  // buffer only between blocks), the zero bands replaced by one zero row zrow
   constexpr int kBndLen = COLS ? 2 * (NB + 2) * 2 * HW * QW : 0;
-  unsigned long long* red = (unsigned long long*)(bnd + kBndLen);  // [3]
+  double2* bnd = CW ? (double2*)bufA : (double2*)(snap + (MODE == kModeFwd ? a.emax : 0));
+  unsigned char* tail = CW ? (unsigned char*)bufA + max((size_t)blen * sizeof(double), (size_t)kBndLen * sizeof(double2))
+                           : (unsigned char*)(bnd + kBndLen);
+  double2* wmid = (double2*)tail;                                        // CW: [NB][RW][HW] middle columns' w_0 per band row (0 off rows 0 / H - 1)
+  double2* zrow = wmid + (CW ? NB * RW * HW : 0);                        // CW: [HW][QW] zeros
+  unsigned long long* red = (unsigned long long*)(zrow + (CW ? HW * QW : 0));  // [3]
   int* lflag = (int*)(red + 3);                                          // [4]
 
   const size_t iS = (size_t)inst * S;
@@ -184,31 +214,73 @@ __global__ void __launch_bounds__(NT) cluster_kernel(ClusterArgs a) {
   }
 
   // ---- per-state constants into registers --------------------------------
-  double w[SPT][kStencilK];     // forward: gather weights; backward: reward-folded weights
+  double w[CW ? 1 : SPT][kStencilK];  // forward: gather weights; backward: reward-folded weights
+  double wc[CW ? SPT : 1][3];         // CW: w_x (both horizontal neighbours), w_+y, w_-y
+  double edge_w[CW ? 2 * RW : 1];     // CW: per band row, w_0 of columns 0 / CPL-1 (x-border lanes, border rows; else 0)
   double c0[MODE == kModeFwd ? SPT : 1];  // forward: p0
   const size_t wbase = iS * kStencilK;
 #pragma unroll
   for (int j = 0; j < SPT; ++j) {
     const int l = slot_state(j);
     if (MODE == kModeFwd) c0[MODE == kModeFwd ? j : 0] = 0.0;
+    if constexpr (CW) {
 #pragma unroll
-    for (int k = 0; k < kStencilK; ++k) w[j][k] = 0.0;
-    if (l < E) {
-      const int s = base + l;
-      if (MODE == kModeFwd) c0[MODE == kModeFwd ? j : 0] = a.vin[iS + s];
+      for (int k = 0; k < 3; ++k) wc[j][k] = 0.0;
+      if (l < E) {
+        const int s = base + l;
+        const int x = s % W;
+        wc[j][0] = a.wgt[wbase + (size_t)(x + 1 < W ? 1 : 2) * S + s];
+        wc[j][1] = a.wgt[wbase + (size_t)3 * S + s];
+        wc[j][2] = a.wgt[wbase + (size_t)4 * S + s];
+      }
 #pragma unroll
-      for (int k = 0; k < kStencilK; ++k) w[j][k] = a.wgt[wbase + (size_t)k * S + s];
+      for (int k = 0; k < 3; ++k) asm volatile("" : "+v"(wc[j][k]));
+    } else {
+#pragma unroll
+      for (int k = 0; k < kStencilK; ++k) w[j][k] = 0.0;
+      if (l < E) {
+        const int s = base + l;
+        if (MODE == kModeFwd) c0[MODE == kModeFwd ? j : 0] = a.vin[iS + s];
+#pragma unroll
+        for (int k = 0; k < kStencilK; ++k) w[j][k] = a.wgt[wbase + (size_t)k * S + s];
+      }
+      // pin the constants in registers: without this the compiler re-loads them
+      // from global memory inside every sweep (rematerialisation of invariant loads)
+#pragma unroll
+      for (int k = 0; k < kStencilK; ++k) asm volatile("" : "+v"(w[j][k]));
+      if (MODE == kModeFwd) asm volatile("" : "+v"(c0[MODE == kModeFwd ? j : 0]));
     }
-    // pin the constants in registers: without this the compiler re-loads them
-    // from global memory inside every sweep (rematerialisation of invariant loads)
+  }
+  if constexpr (CW) {
 #pragma unroll
-    for (int k = 0; k < kStencilK; ++k) asm volatile("" : "+v"(w[j][k]));
-    if (MODE == kModeFwd) asm volatile("" : "+v"(c0[MODE == kModeFwd ? j : 0]));
+    for (int r = 0; r < RW; ++r) {
+      edge_w[2 * r] = 0.0;
+      edge_w[2 * r + 1] = 0.0;
+      const int l0 = slot_state(r * CPL), l3 = slot_state(r * CPL + CPL - 1);
+      const int y = e0 + l0 / W;
+      const bool brow = l0 < E && (y == 0 || y == H - 1);
+      if ((cp == 0 || brow) && l0 < E) edge_w[2 * r] = a.wgt[wbase + base + l0];
+      if ((cp == HW - 1 || brow) && l3 < E) edge_w[2 * r + 1] = a.wgt[wbase + base + l3];
+      asm volatile("" : "+v"(edge_w[2 * r]));
+      asm volatile("" : "+v"(edge_w[2 * r + 1]));
+    }
   }
   // one sweep's new value from the weighted sum: forward p0 + sum, backward the sum
   auto finish = [&](int j, double acc) { return MODE == kModeFwd ? c0[MODE == kModeFwd ? j : 0] + acc : acc; };
   for (int i = tid; i < (COLS ? 1 : 2) * blen; i += NT) bufA[i] = 0.0;
   for (int i = tid; i < kBndLen; i += NT) bnd[i] = make_double2(0.0, 0.0);
+  if constexpr (CW) {
+    static_assert(!CW || CPL == 4, "compact weights: column quads");
+    for (int i = tid; i < HW * QW; i += NT) zrow[i] = make_double2(0.0, 0.0);
+#pragma unroll
+    for (int r = 0; r < RW; ++r) {  // w_0 of columns 1, 2 of this lane's band row r: nonzero on rows 0 / H - 1 only
+      const int l1 = slot_state(r * CPL + 1);
+      const int y = e0 + l1 / W;
+      const bool brow = l1 < E && (y == 0 || y == H - 1);
+      wmid[(bb * RW + r) * HW + cp] = brow ? make_double2(a.wgt[wbase + base + l1], a.wgt[wbase + base + l1 + 1])
+                                           : make_double2(0.0, 0.0);
+    }
+  }
   __syncthreads();
   for (int l = tid; l < E; l += NT) {
     double v0 = 0.0;
@@ -316,8 +388,8 @@ __global__ void __launch_bounds__(NT) cluster_kernel(ClusterArgs a) {
         const double va = cv[2 * jp], vb = cv[2 * jp + 1];
         const double lft = dpp_shift_f64<0x138>(vb);  // wave_shr1: left neighbour of state a
         const double rgt = dpp_shift_f64<0x130>(va);  // wave_shl1: right neighbour of state b
-        const double* wa = w[2 * jp];
-        const double* wb = w[2 * jp + 1];
+        const double* wa = w[CW ? 0 : 2 * jp];
+        const double* wb = w[CW ? 0 : 2 * jp + 1];
         double acc = fma(wa[0], va, 0.0);
         acc = fma(wa[1], vb, acc);
         acc = fma(wa[2], lft, acc);
@@ -342,11 +414,11 @@ __global__ void __launch_bounds__(NT) cluster_kernel(ClusterArgs a) {
         const int l = tid + j * NT;
         const double* q = din + l + 1;
         const double self = q[W];
-        double acc = fma(w[j][0], self, 0.0);
-        acc = fma(w[j][1], q[W + 1], acc);
-        acc = fma(w[j][2], q[W - 1], acc);
-        acc = fma(w[j][3], q[2 * W], acc);
-        acc = fma(w[j][4], q[0], acc);
+        double acc = fma(w[CW ? 0 : j][0], self, 0.0);
+        acc = fma(w[CW ? 0 : j][1], q[W + 1], acc);
+        acc = fma(w[CW ? 0 : j][2], q[W - 1], acc);
+        acc = fma(w[CW ? 0 : j][3], q[2 * W], acc);
+        acc = fma(w[CW ? 0 : j][4], q[0], acc);
         const double nv = finish(j, acc);
         dout[pad + l] = nv;
         account(j, nv, self);
@@ -379,6 +451,17 @@ __global__ void __launch_bounds__(NT) cluster_kernel(ClusterArgs a) {
     if constexpr (COLS) {
       const unsigned ob = slot_bits(own_bits);
       double dmax = 0.0;
+#ifndef IRLMX_CW_PREFETCH
+#define IRLMX_CW_PREFETCH 1
+#endif
+      // CW: the middle columns' self weights of every row, read at the top of
+      // the sweep (constant LDS data: ahead of the edge-row stores and the
+      // barrier) so that no row's FMA chain starts by waiting for its read
+      double2 wm_pf[CW && IRLMX_CW_PREFETCH ? RW : 1];
+      if constexpr (CW && IRLMX_CW_PREFETCH) {
+#pragma unroll
+        for (int r = 0; r < RW; ++r) wm_pf[r] = wmid[(bb * RW + r) * HW + cp];
+      }
 #ifndef IRLMX_FWD_BRANCH_ACCOUNT
 #define IRLMX_FWD_BRANCH_ACCOUNT 1
 #endif
@@ -457,8 +540,8 @@ __global__ void __launch_bounds__(NT) cluster_kernel(ClusterArgs a) {
           }
           return;
         }
-        const double2* t = bnd_at(i & 1, bb, 1);
-        const double2* u = bnd_at(i & 1, bb + 2, 0);
+        const double2* t = (CW && bb == 0) ? zrow + cp * QW : bnd_at(i & 1, bb, 1);
+        const double2* u = (CW && bb == NB - 1) ? zrow + cp * QW : bnd_at(i & 1, bb + 2, 0);
 #pragma unroll
         for (int q = 0; q < QW; ++q) {
           if (which & 1) {
@@ -494,16 +577,34 @@ __global__ void __launch_bounds__(NT) cluster_kernel(ClusterArgs a) {
           const double lft = edge_row ? side[er][0] : dpp_shift_f64<0x138>(v[CPL - 1]);  // wave_shr1: left of column 0
           const double rgt = edge_row ? side[er][1] : dpp_shift_f64<0x130>(v[0]);        // wave_shl1: right of column CPL - 1
           double acc[CPL];
+          if constexpr (CW) {
+            // the five-weight chain with w_1 = w_2 = w_x and the self term as
+            // described at the top of the kernel
+            const double2 wm = IRLMX_CW_PREFETCH ? wm_pf[IRLMX_CW_PREFETCH ? jr : 0] : wmid[(bb * RW + jr) * HW + cp];
+            acc[0] = fma(edge_w[2 * jr], v[0], 0.0);
+            acc[1] = fma(wm.x, v[1], 0.0);
+            acc[2] = fma(wm.y, v[2], 0.0);
+            acc[CPL - 1] = fma(edge_w[2 * jr + 1], v[CPL - 1], 0.0);
 #pragma unroll
-          for (int c = 0; c < CPL; ++c) acc[c] = fma(w[jr * CPL + c][0], v[c], 0.0);
+            for (int c = 0; c < CPL; ++c) acc[c] = fma(wc[jr * CPL + c][0], c + 1 < CPL ? v[c + 1 < CPL ? c + 1 : 0] : rgt, acc[c]);
 #pragma unroll
-          for (int c = 0; c < CPL; ++c) acc[c] = fma(w[jr * CPL + c][1], c + 1 < CPL ? v[c + 1 < CPL ? c + 1 : 0] : rgt, acc[c]);
+            for (int c = 0; c < CPL; ++c) acc[c] = fma(wc[jr * CPL + c][0], c > 0 ? v[c > 0 ? c - 1 : 0] : lft, acc[c]);
 #pragma unroll
-          for (int c = 0; c < CPL; ++c) acc[c] = fma(w[jr * CPL + c][2], c > 0 ? v[c > 0 ? c - 1 : 0] : lft, acc[c]);
+            for (int c = 0; c < CPL; ++c) acc[c] = fma(wc[jr * CPL + c][1], dn[c], acc[c]);
 #pragma unroll
-          for (int c = 0; c < CPL; ++c) acc[c] = fma(w[jr * CPL + c][3], dn[c], acc[c]);
+            for (int c = 0; c < CPL; ++c) acc[c] = fma(wc[jr * CPL + c][2], up[c], acc[c]);
+          } else {
 #pragma unroll
-          for (int c = 0; c < CPL; ++c) acc[c] = fma(w[jr * CPL + c][4], up[c], acc[c]);
+            for (int c = 0; c < CPL; ++c) acc[c] = fma(w[CW ? 0 : jr * CPL + c][0], v[c], 0.0);
+#pragma unroll
+            for (int c = 0; c < CPL; ++c) acc[c] = fma(w[CW ? 0 : jr * CPL + c][1], c + 1 < CPL ? v[c + 1 < CPL ? c + 1 : 0] : rgt, acc[c]);
+#pragma unroll
+            for (int c = 0; c < CPL; ++c) acc[c] = fma(w[CW ? 0 : jr * CPL + c][2], c > 0 ? v[c > 0 ? c - 1 : 0] : lft, acc[c]);
+#pragma unroll
+            for (int c = 0; c < CPL; ++c) acc[c] = fma(w[CW ? 0 : jr * CPL + c][3], dn[c], acc[c]);
+#pragma unroll
+            for (int c = 0; c < CPL; ++c) acc[c] = fma(w[CW ? 0 : jr * CPL + c][4], up[c], acc[c]);
+          }
 #pragma unroll
           for (int c = 0; c < CPL; ++c) {
             dst[jr * CPL + c] = finish(jr * CPL + c, acc[c]);
@@ -551,9 +652,15 @@ __global__ void __launch_bounds__(NT) cluster_kernel(ClusterArgs a) {
   };
 
   // Halo exchange in tagged granules (cluster.h): this instance's region of
-  // a.gran is [2 parities][S states] x 16 B, of a.sgran [kSumSlots + 1][H tiles] x 16 B
+  // a.gran is [2 parities][H rows][W + kGranRowPad] x 16 B (cluster.h), of a.sgran [kSumSlots + 1][H tiles] x 16 B
   // (summaries by block % kSumSlots, then the XCC ids).
-  const Gran rg = gran_rsrc(a.gran + (size_t)inst * 4 * S, 32u * (unsigned)S);
+  const size_t gpl = gran_par_len(W, H);
+  const Gran rg = gran_rsrc(a.gran + (size_t)inst * 2 * gran_inst_len(W, H), 32u * (unsigned)gpl);
+  constexpr int kRG = WT ? WT + kGranRowPad : 0;  // granules per row (compile-time where the width is)
+  const unsigned rgw = WT ? kRG : (unsigned)(W + kGranRowPad);
+  const unsigned gbase = (unsigned)e0 * rgw;
+  // granule index of extended-tile state l in the parity-0 half
+  auto gidx = [&](int l) { return gbase + (unsigned)(l / W) * rgw + (unsigned)(l % W); };
   const Gran rs = gran_rsrc(a.sgran + (size_t)inst * 2 * (kSumSlots + 1) * a.H, 16u * (kSumSlots + 1) * (unsigned)a.H);
   const int ng0 = own0, ng = own0 + (E - own1);  // ghost states: [0, own0) and [own1, E)
   const unsigned salt = (a.salt & 0xFFFu) << 20;  // per call: a stale granule of an earlier call never matches
@@ -682,7 +789,7 @@ __global__ void __launch_bounds__(NT) cluster_kernel(ClusterArgs a) {
     if (stamps) st_acc[4] += 1;
     // ---- publish the halo rows, tagged with the block ------------------------
     const unsigned tag = salt | (((unsigned)m + 1u) & 0xFFFFFu);
-    const unsigned gpar = (unsigned)(m & 1) * (unsigned)S;
+    const unsigned gpar = (unsigned)(m & 1) * (unsigned)gpl;
     // one tile per instance (C == 1: a 64x64 grid fits one CU): no halo, the
     // block summary is the tile's own -- no hand-off at all.  (Compiled in for
     // width 64 only: wider grids never fit one tile, and their kernels keep the
@@ -690,9 +797,9 @@ __global__ void __launch_bounds__(NT) cluster_kernel(ClusterArgs a) {
     const bool solo = WT == 64 && a.C == 1;
     auto store_rows = [&]() {  // from the LDS tile, spread evenly over all threads
       for (int l = own0 + tid; l < pubA1; l += NT)
-        gran_store(rg, (gpar + (unsigned)(base + l)) * 16u, dbits(cur[pad + l]), tag, plain);
+        gran_store(rg, (gpar + gidx(l)) * 16u, dbits(cur[pad + l]), tag, plain);
       for (int l = pubB0 + tid; l < own1; l += NT)
-        gran_store(rg, (gpar + (unsigned)(base + l)) * 16u, dbits(cur[pad + l]), tag, plain);
+        gran_store(rg, (gpar + gidx(l)) * 16u, dbits(cur[pad + l]), tag, plain);
     };
     if constexpr (COLS) {
       // a band's rows sit in one wave: stage them in the LDS tile first, so that
@@ -711,7 +818,7 @@ __global__ void __launch_bounds__(NT) cluster_kernel(ClusterArgs a) {
 #pragma unroll
       for (int j = 0; j < SPT; ++j)  // per register slot: all stores of a thread in flight together
         if ((pb >> j) & 1u)
-          gran_store(rg, (gpar + (unsigned)(base + slot_state(j))) * 16u, dbits(cv[PAIR ? j : 0]), tag, plain);
+          gran_store(rg, (gpar + gidx(slot_state(j))) * 16u, dbits(cv[PAIR ? j : 0]), tag, plain);
     } else {
       store_rows();
     }
@@ -758,7 +865,7 @@ __global__ void __launch_bounds__(NT) cluster_kernel(ClusterArgs a) {
           }
 #pragma unroll
           for (int i = 0; i < kPub; ++i)
-            if (ls[i] >= 0) gran_store(rg, (gpar + (unsigned)(base + ls[i])) * 16u, dbits(vv[i]), tag, plain);
+            if (ls[i] >= 0) gran_store(rg, (gpar + gidx(ls[i])) * 16u, dbits(vv[i]), tag, plain);
         }
       }
     }
@@ -782,7 +889,7 @@ __global__ void __launch_bounds__(NT) cluster_kernel(ClusterArgs a) {
         for (int i = 0; i < GPT; ++i) {
           const int k = k0 + tid + i * NT;
           ls[i] = k < ng0 ? k : own1 + (k - ng0);
-          off[i] = (gpar + (unsigned)(base + ls[i])) * 16u;
+          off[i] = (gpar + gidx(ls[i])) * 16u;
           want |= (k < ng ? 1u : 0u) << i;
         }
         off[GPT] = ((unsigned)(m % kSumSlots) * (unsigned)a.H + (unsigned)tid) * 16u;
@@ -949,6 +1056,30 @@ __global__ void bwd_growth_kernel(const double* __restrict__ bw, int S, int B, u
   }
 }
 
+// Does the backward of these STENCIL5 tables fit the compact-weight layout
+// (cluster_kernel LAY == 4)?  With c_k(s) = sum_a row_val[a][k][s] summed as
+// bwd_weights_kernel sums it (so the reward-folded weights inherit every
+// equality): c_+x == c_-x wherever both neighbours are in the grid, and
+// c_self == 0 off the grid border.  Any violation sets *bad.  One block row of
+// threads per table instance (grid.y).
+__global__ void bwd_compact_ok_kernel(const double* __restrict__ row_val, int W, int H, int A, int* __restrict__ bad) {
+  const int s = blockIdx.x * blockDim.x + threadIdx.x;
+  const int S = W * H;
+  if (s >= S) return;
+  const double* rv = row_val + (size_t)blockIdx.y * A * kStencilK * S;
+  double c[kStencilK];
+  for (int k = 0; k < kStencilK; ++k) {
+    double acc = 0.0;
+    for (int a = 0; a < A; ++a) acc += rv[((size_t)a * kStencilK + k) * S + s];
+    c[k] = acc;
+  }
+  const int x = s % W, y = s / W;
+  const bool ix = x > 0 && x < W - 1, iy = y > 0 && y < H - 1;
+  bool ok = !ix || (dbits(c[1]) == dbits(c[2]));
+  if (ix && iy) ok = ok && dbits(c[0]) == 0ull;
+  if (!ok) atomicOr(bad, 1);
+}
+
 static std::atomic<unsigned> g_salt{1};  // per-launch tag salt (cluster.h granules)
 
 static int env_int(const char* name, int dflt) {
@@ -985,8 +1116,15 @@ static size_t cluster_lds(int emax, int W, int layout, int nt, int mode) {
   if (layout >= 2) {
     // column strips: one tile buffer (ghost staging, final sweep) + snapshot +
     // band edge rows [2][NB + 2][2][W / CPL lanes] of CPL doubles + summary words
-    const int cpl = layout == 3 ? 4 : 2;
+    const int cpl = layout >= 3 ? 4 : 2;
     const size_t bnd = 2 * (size_t)(nt / (W / cpl) + 2) * 2 * W * sizeof(double);
+    if (layout == 4) {
+      // compact weights: the edge rows alias the tile buffer (the kernel's
+      // padded buffer is emax + 2 W doubles); + the middle columns' self
+      // weights per band row (16 B per lane and row) and one zero edge row
+      const size_t tb = (size_t)(emax + 2 * W) * sizeof(double);
+      return std::max(tb, bnd) + (size_t)emax / 4 * 16 + W * sizeof(double) + 64;
+    }
     return buf + snap + bnd + 64;
   }
   // ping-pong buffers + snapshot + summary words
@@ -996,7 +1134,7 @@ static size_t cluster_lds(int emax, int W, int layout, int nt, int mode) {
 // Tile plan for a width x height stencil grid and B instances: the fewest
 // sequential launches first, then the most sweeps per exchange (G), then the
 // smallest extended tile.  IRLMX_CLUSTER_R / _G force a plan (tests).
-bool cluster_plan(int W, int H, int B, int mode, ClusterPlan* out) {
+bool cluster_plan(int W, int H, int B, int mode, ClusterPlan* out, bool compact) {
   if (env_int("IRLMX_CLUSTER", 1) == 0) return false;
   const int cus = plan_cus();
   if (cus <= 0) return false;
@@ -1009,12 +1147,18 @@ bool cluster_plan(int W, int H, int B, int mode, ClusterPlan* out) {
   if (W == 64 || W == 128) layout = env_layout >= 0 ? std::min(env_layout, W == 128 ? 3 : 2) : 2;
   // (the forward's column quads fit only 8 states per lane: too few rows per
   // tile at width 256, so its forward stays per state)
-  if (W == 256) layout = env_layout >= 0 ? (env_layout == 3 ? 3 : 0) : (mode == kModeBwd ? 3 : 0);
+  // (compact: the backward's tables fit layout 4, column quads with three
+  // weights per state -- checked per call; IRLMX_PAIR=3 forces the five-weight quads)
+  const bool cw = compact && W == 256 && mode == kModeBwd && env_int("IRLMX_COMPACT", 1) != 0;
+  if (W == 256)
+    layout = env_layout >= 0 ? (env_layout == 4 && cw ? 4 : (env_layout >= 3 ? 3 : 0))
+                             : (mode == kModeBwd ? (cw ? 4 : 3) : 0);
   const bool pair = layout > 0;
   const int nt = pair ? kPairThreads : kCT;
   // register budget per lane: the forward's convergence bookkeeping needs more
   // (IRLMX_SPT_MAX: experiments only)
   const int spt_max = env_int("IRLMX_SPT_MAX", !pair ? kSptMax
+                                              : layout == 4 ? kSptMaxQuadBwdCW
                                               : layout == 3 ? (mode == kModeFwd ? kSptMaxQuadFwd : kSptMaxQuadBwd)
                                                             : kSptMaxPair);
   const int rows_cap = nt * spt_max / W;
@@ -1028,7 +1172,7 @@ bool cluster_plan(int W, int H, int B, int mode, ClusterPlan* out) {
       const int ext = std::min(H, R + 2 * G);
       const int E = ext * W;
       int spt = (E + nt - 1) / nt;
-      if (pair) spt = (spt + (layout == 3 ? 3 : 1)) / (layout == 3 ? 4 : 2) * (layout == 3 ? 4 : 2);
+      if (pair) spt = (spt + (layout >= 3 ? 3 : 1)) / (layout >= 3 ? 4 : 2) * (layout >= 3 ? 4 : 2);
       if (spt > spt_max) continue;
       const size_t lds = cluster_lds(spt * nt, W, layout, nt, mode);
       if (lds + kClusterStaticLds > kMaxLdsBytes) continue;
@@ -1112,6 +1256,18 @@ static void* cluster_fn_quad(int spt) {
 
 template <int MODE>
 static void* cluster_fn(int spt, int W, int layout, int) {
+  if (layout == 4) {
+    if constexpr (MODE == kModeBwd) {
+      if (W != 256) return nullptr;
+      switch (spt) {
+        case 8: return (void*)&cluster_kernel<MODE, 8, 256, 4, kPairThreads>;
+        case 12: return (void*)&cluster_kernel<MODE, 12, 256, 4, kPairThreads>;
+        case 16: return (void*)&cluster_kernel<MODE, 16, 256, 4, kPairThreads>;
+        case 20: return (void*)&cluster_kernel<MODE, 20, 256, 4, kPairThreads>;
+      }
+    }
+    return nullptr;
+  }
   if (layout == 3) {
     if (W == 128) return cluster_fn_quad<MODE, 128>(spt);
     if (W == 256) return cluster_fn_quad<MODE, 256>(spt);
@@ -1195,7 +1351,7 @@ int cluster_run(int mode, const ClusterPlan& plan, ClusterArgs a, int B, hipStre
     for (int g = 0; g < nwg; ++g)
       for (int k = 0; k < 8; ++k) acc[k] += (double)h[(size_t)g * 8 + k] / nwg;
     fprintf(stderr, "[irlmx stamps] %s%s mode=%d R=%d G=%d C=%d spt=%d blocks=%.0f  cycles/block: sweeps %.0f  publish %.0f  "
-                    "wait %.0f  refresh %.0f  same-xcd %.2f  (publish: stores %.0f, summary %.0f)\n", "lds", p.pair == 3 ? "-quads" : (p.pair == 2 ? "-cols" : (p.pair == 1 ? "-pair" : "")), mode, p.R, p.G, p.C, p.spt,
+                    "wait %.0f  refresh %.0f  same-xcd %.2f  (publish: stores %.0f, summary %.0f)\n", "lds", p.pair == 4 ? "-quads-cw" : p.pair == 3 ? "-quads" : (p.pair == 2 ? "-cols" : (p.pair == 1 ? "-pair" : "")), mode, p.R, p.G, p.C, p.spt,
             acc[4], acc[0] / acc[4], acc[1] / acc[4], acc[2] / acc[4], acc[3] / acc[4], acc[5], acc[6] / acc[4],
             (acc[7] - acc[6]) / acc[4]);
     if (p.C <= 8) {  // per tile position: the interior tiles carry ghost rows on both sides

@@ -176,10 +176,11 @@ static Ws carve(const Model& m, int op, void* base) {
   const bool gr = sweep && grid_plan(m, op, &gp);
   DenseGridPlan dp{0, 0, 0, 0};
   const bool dg = sweep && dense_grid(m, op, &dp);
-  // cluster halo exchange: [B][2][S] and [B][kSumSlots + 1][H] 16-byte granule pairs;
+  // cluster halo exchange: [B][gran_inst_len] and [B][kSumSlots + 1][H] 16-byte granule pairs;
   // grid shape: [B][3][S] value and [B][3][bpi] block-delta granules;
   // dense grid shape: [B][2][S] value and [B][bpi] XCC-id granules
-  w.gran = (unsigned long long*)take(cl || dg ? 2 * B * S * 16 : (gr ? 3 * B * S * 16 : 0));
+  const size_t gcl = cl ? B * gran_inst_len(m.W, m.H) * 16 : 0;   // cluster.h kGranRowPad layout
+  w.gran = (unsigned long long*)take(std::max(gcl, dg ? 2 * B * S * 16 : (gr ? 3 * B * S * 16 : 0)));
   w.sgran = (unsigned long long*)take(cl ? (kSumSlots + 1) * B * (size_t)m.H * 16
                                          : (gr ? 4 * B * (size_t)gp.bpi * 16 : (dg ? B * (size_t)dp.bpi * 16 : 0)));
   w.growth = (unsigned long long*)take(cl ? 2 * B * sizeof(unsigned long long) : 0);
@@ -2522,6 +2523,23 @@ extern "C" int irlmx_dense_to_rows(const double* dense, int32_t n_states, int32_
   return e == hipSuccess ? 0 : hip_fail(e, "dense_to_rows");
 }
 
+namespace irlmx {
+// The backward's tables fit the compact-weight cluster layout (cluster.hip,
+// LAY 4: width 256 only)?  Checked on the device per call
+// (bwd_compact_ok_kernel), one int of device memory as the flag; synchronises
+// the stream.  IRLMX_COMPACT=0 turns the layout off.
+static bool bwd_compact(const Model& m, int* flag, hipStream_t st) {
+  if (!m.stencil || m.W != 256 || getenv_int("IRLMX_COMPACT", 1) == 0) return false;
+  if (hipMemsetAsync(flag, 0, sizeof(int), st) != hipSuccess) return false;
+  hipLaunchKernelGGL(bwd_compact_ok_kernel, dim3((m.S + 255) / 256, m.shared ? 1 : m.B), dim3(256), 0, st,
+                     m.row_val, m.W, m.H, m.A, flag);
+  int h = 1;
+  if (hipMemcpyAsync(&h, flag, sizeof(int), hipMemcpyDeviceToHost, st) != hipSuccess) return false;
+  if (hipStreamSynchronize(st) != hipSuccess) return false;
+  return h == 0;
+}
+}  // namespace irlmx
+
 extern "C" size_t irlmx_workspace_bytes(const irlmx_mdp* mdp, int32_t op) {
   if (validate(mdp)) return 0;
   return carve(make_model(mdp), op, nullptr).total;
@@ -2548,8 +2566,16 @@ extern "C" int irlmx_execution_plan(const irlmx_mdp* mdp, int32_t op, int64_t* p
   }
   ClusterPlan cp;
   const int mode = op == IRLMX_OP_FORWARD ? kModeFwd : kModeBwd;
+  bool compact = false;
+  if (op == IRLMX_OP_BACKWARD && m.stencil && m.W == 256) {  // (data-dependent: the table's structure)
+    int* flag = nullptr;
+    if (hipMalloc((void**)&flag, sizeof(int)) == hipSuccess) {
+      compact = bwd_compact(m, flag, nullptr);
+      (void)hipFree(flag);
+    }
+  }
   if (m.stencil && (op == IRLMX_OP_FORWARD || (op == IRLMX_OP_BACKWARD && !no_rescale && m.A <= kMaxActions)) &&
-      cluster_plan(m.W, m.H, m.B, mode, &cp)) {
+      cluster_plan(m.W, m.H, m.B, mode, &cp, compact)) {
     plan[0] = IRLMX_SHAPE_CLUSTER;
     plan[1] = cp.R; plan[2] = cp.G; plan[3] = cp.C; plan[4] = cp.per_launch; plan[5] = cp.spt;
     plan[6] = cp.pair; plan[7] = cp.nt; plan[8] = (m.B + cp.per_launch - 1) / cp.per_launch;
@@ -2702,7 +2728,8 @@ extern "C" int irlmx_backward_maxent(const irlmx_mdp* mdp, const double* reward,
   bool persistent = true;  // false once a persistent launch found its workgroups not co-resident
   // (without rescaling the partition vector overflows like the reference's: such
   // calls take the per-sweep shape, whose non-finite bookkeeping is per sweep)
-  if (m.stencil && m.A <= kMaxActions && rescale && cluster_plan(m.W, m.H, m.B, kModeBwd, &cp)) {
+  if (m.stencil && m.A <= kMaxActions && rescale &&
+      cluster_plan(m.W, m.H, m.B, kModeBwd, &cp, m.W == 256 && bwd_compact(m, ws.err + 3, st))) {
     hipLaunchKernelGGL(bwd_growth_kernel, dim3(m.B), dim3(1024), 0, st, ws.wgt, m.S, m.B, ws.growth);
     ClusterArgs ca{};
     ca.W = m.W; ca.H = m.H; ca.S = m.S; ca.A = m.A;

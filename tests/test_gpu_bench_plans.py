@@ -30,8 +30,8 @@ CONTRACT = 1e-5
 # plans of the bench workloads on one MI355X (256 CUs); bench.py reports them in
 # its JSON line ("plans").  Keys: irlmx.ops.PLAN_FIELDS.
 C3_BWD_PLAN = {"shape": "cluster", "R": 32, "G": 8, "C": 4, "per_launch": 64, "spt": 12, "layout": 2, "launches": 1}
-C4_BWD_PLAN = {"shape": "cluster", "R": 16, "G": 8, "C": 16, "per_launch": 16, "spt": 16, "layout": 3,
-               "launches": 2}
+C4_BWD_PLAN = {"shape": "cluster", "R": 32, "G": 4, "C": 8, "per_launch": 32, "spt": 20, "layout": 4,
+               "launches": 1}
 
 
 def rel_err(got, ref):
@@ -147,9 +147,10 @@ def test_config3_bench_plan_three_irl_steps(dev):
 
 
 def test_config4_bench_plan_two_irl_steps(dev):
-    """Config 4: 256x256, 32 instances per GPU -- backward plan R=16 / G=8 / C=16,
-    16 states per lane in column quads, two sequential launches; two gradient
-    steps for b = 0 and 31 (vectors checked on 4,096 states + whole-vector sums)."""
+    """Config 4: 256x256, 32 instances per GPU -- backward plan R=32 / G=4 / C=8,
+    20 states per lane in column quads with compact weights (three per state),
+    all 32 instances in one launch; two gradient steps for b = 0 and 31 (vectors
+    checked on 4,096 states + whole-vector sums)."""
     from irlmx import ops
     z, checked, mdp, steps = run_bench_workload(dev, "c4", 256, 32, 2)
     assert plan_subset(ops.execution_plan(mdp, "backward"), C4_BWD_PLAN) == C4_BWD_PLAN
@@ -212,9 +213,9 @@ def test_config3_timed_steps_plan_independent(dev):
 
 
 def test_config4_full_vectors_plan_independent(dev):
-    """Config 4's benchmarked plan (B = 32: R=16 / G=8 / C=16, two sequential
-    launches) against instances 0 and 31 run alone (B = 2: a different tile
-    count per instance, one launch): the whole policy (65,536 x 4) and SVF
+    """Config 4's benchmarked plan (B = 32: R=32 / G=4 / C=8, compact weights,
+    one launch) against instances 0 and 31 run alone (B = 2: a different tile
+    count per instance): the whole policy (65,536 x 4) and SVF
     (65,536) vectors, sweep counts and theta equal bit for bit for two gradient
     steps.  Complements test_config4_bench_plan_two_irl_steps, whose fixture holds
     4,096 states per vector plus whole-vector sums; with
@@ -268,3 +269,68 @@ def test_backward_lazy_summary_bit_identical(dev, monkeypatch, size, B):
     eager = ops.backward_maxent(mdp, r, tm)
     assert bool(torch.isfinite(lazy).all())
     assert torch.equal(lazy, eager)
+
+
+def test_config3_whole_irl_run_against_oracle(dev):
+    """A whole config-3 ``irl`` run (maxent.py:236-255, eps = 1e-4) on the
+    benchmarked B = 64 plan, as ``bench.py``'s ``full_run`` does it
+    (BatchedMaxEnt.run with compaction), against the CPU oracle run to the
+    reference's own stopping rule for instances 0 and 63
+    (tests/golden/run_c3.npz, tools/gen_full_fixtures.py c3run, ~2.5 h each):
+    gradient-step count and every step's forward sweep count identical; theta
+    after steps 1, 2, 3, 6, 15, 25 (the bench's timed window at W = 5, K = 20)
+    and the final reward within 1e-9 relative (contract 1e-5); per-step
+    theta sums within 1e-9."""
+    from irlmx import DeviceMDP, demos, ops
+    from irlmx.batch import BatchedMaxEnt
+    from irlmx.shard import instance_slips
+    try:
+        z = load_golden("run_c3")
+    except FileNotFoundError:
+        pytest.skip("tests/golden/run_c3.npz not generated")
+    size, B, S = 128, 64, 128 * 128
+    checked = [int(b) for b in z["instances"]]
+    slips = instance_slips(np.arange(B), B)
+    mdp = DeviceMDP.icy_gridworld(size, slips, device=dev)
+    assert plan_subset(ops.execution_plan(mdp, "backward"), C3_BWD_PLAN) == C3_BWD_PLAN
+    rv = mdp.row_val.cpu().numpy()
+    e_f = np.empty((B, S))
+    p0 = np.empty((B, S))
+    for b in range(B):
+        e_f[b], p0[b], _ = demos.sample(rv[b], size, [S - 1], 0, n=200, seed=1234 + b, max_len=demos.safety_cap(size))
+    for b in checked:
+        assert float(slips[b]) == float(z[f"{b}__slip"])
+    irl = BatchedMaxEnt(mdp, e_f, p0, [S - 1])
+    rec = {b: {"k_f": [], "theta_sum": [], "at": {}} for b in checked}
+    keep = sorted(int(k.split("theta_at")[1]) for k in z.files if k.startswith(f"{checked[0]}__theta_at"))
+
+    def on_step(m):
+        steps = m.steps.cpu().numpy()
+        kf = m.last_forward_sweeps.cpu().numpy()
+        th = m.theta[checked].cpu().numpy()
+        for j, b in enumerate(checked):
+            if steps[b] == m.k:   # b was active in this step
+                rec[b]["k_f"].append(int(kf[b]))
+                rec[b]["theta_sum"].append([th[j].sum(), np.abs(th[j]).max()])
+                if m.k in keep:
+                    rec[b]["at"][m.k] = th[j].copy()
+
+    reward, steps = irl.run(eps=1e-4, compact=True, on_step=on_step)
+    steps = steps.cpu().numpy()
+    reward = reward.cpu().numpy()
+    for b in checked:
+        key = f"{b}__"
+        ref_kf = z[key + "k_f"]
+        got_kf = np.array(rec[b]["k_f"])
+        n = min(len(ref_kf), len(got_kf))
+        diff = np.flatnonzero(got_kf[:n] != ref_kf[:n])
+        assert diff.size == 0, (b, "forward sweeps differ first at step", int(diff[0]) + 1,
+                                int(got_kf[diff[0]]), int(ref_kf[diff[0]]))
+        assert int(steps[b]) == int(z[key + "steps"]) == len(got_kf), (b, int(steps[b]), int(z[key + "steps"]))
+        ts = np.array(rec[b]["theta_sum"])
+        ref_ts = z[key + "theta_sum"]
+        e = np.max(np.abs(ts - ref_ts) / np.abs(ref_ts))
+        assert e <= RTOL, (b, "theta sums", e)
+        for k in keep:
+            close(rec[b]["at"][k], z[f"{key}theta_at{k}"], (b, "theta", k))
+        close(reward[b], z[key + "theta"], (b, "final reward"))

@@ -654,35 +654,48 @@ def test_solo_backward_rescale_extremes(dev, monkeypatch):
 
 
 def test_width256_quads_bit_identical(dev, monkeypatch):
-    """Width 256 (config 4's grid): column quads (default) == per-state LDS
-    layout == per-sweep shape, bit for bit, backward and a capped forward, two
-    instances."""
+    """Width 256 (config 4's grid): column quads with compact weights (default
+    for gridworld tables: three weights per state, cluster.hip LAY 4), the
+    five-weight column quads (IRLMX_COMPACT=0), the per-state LDS layout and
+    the per-sweep shape, bit for bit, backward and a capped forward, two
+    instances with rewards of both signs (rescaling up and down) -- and a table
+    the compact layout does not fit (the "stay" action: self weights inside the
+    grid), which the planner keeps on the five-weight quads."""
     from irlmx import DeviceMDP, ops
     size, B = 256, 2
     n = size * size
-    mdp = DeviceMDP.icy_gridworld(size, [0.15, 0.3], device=dev)
+    base = DeviceMDP.icy_gridworld(size, [0.15, 0.3], device=dev)
     rng = np.random.default_rng(8)
-    r = rng.uniform(0.0, 1.0, (B, n))
+    r = rng.uniform(-1.0, 1.0, (B, n))
     tm = ops.terminal_mask([n - 1], n, batch=B, device=dev)
     p0 = np.zeros((B, n))
     p0[:, 0] = 1.0
-    keys = ("IRLMX_FUSED_MAX_STATES", "IRLMX_CLUSTER", "IRLMX_CLUSTER_R", "IRLMX_CLUSTER_G", "IRLMX_PAIR")
-    out = {}
-    for name, env in (("sweep", {"IRLMX_CLUSTER": "0"}), ("lds", {"IRLMX_PAIR": "0"}), ("quads", {}),
-                      ("quads_small", {"IRLMX_CLUSTER_R": "5", "IRLMX_CLUSTER_G": "3"})):
+    keys = ("IRLMX_FUSED_MAX_STATES", "IRLMX_CLUSTER", "IRLMX_CLUSTER_R", "IRLMX_CLUSTER_G", "IRLMX_PAIR",
+            "IRLMX_COMPACT")
+    shapes = (("sweep", {"IRLMX_CLUSTER": "0"}), ("lds", {"IRLMX_PAIR": "0"}), ("quads", {"IRLMX_COMPACT": "0"}),
+              ("compact", {}), ("compact_small", {"IRLMX_CLUSTER_R": "5", "IRLMX_CLUSTER_G": "3"}),
+              ("compact_g8", {"IRLMX_CLUSTER_R": "24", "IRLMX_CLUSTER_G": "8"}))
+    for mdp, stay in ((base, False), (base.with_stay(), True)):
+        out = {}
+        for name, env in shapes:
+            if stay and name not in ("sweep", "compact"):
+                continue
+            for k in keys:
+                monkeypatch.delenv(k, raising=False)
+            for k, v in env.items():
+                monkeypatch.setenv(k, v)
+            plan = ops.execution_plan(mdp, "backward")
+            if name.startswith("compact"):
+                assert plan["layout"] == (3 if stay else 4), (name, stay, plan)
+            pi = ops.backward_maxent(mdp, r, tm)
+            svf, k, st = ops.forward_svf(mdp, p0, tm, pi, max_iter=2500)
+            out[name] = (pi, svf, k)
         for k in keys:
             monkeypatch.delenv(k, raising=False)
-        for k, v in env.items():
-            monkeypatch.setenv(k, v)
-        pi = ops.backward_maxent(mdp, r, tm)
-        svf, k, st = ops.forward_svf(mdp, p0, tm, pi, max_iter=2500)
-        out[name] = (pi, svf, k)
-    for k in keys:
-        monkeypatch.delenv(k, raising=False)
-    for name in ("lds", "quads", "quads_small"):
-        assert torch.equal(out["sweep"][0], out[name][0]), (name, "pi")
-        assert torch.equal(out["sweep"][1], out[name][1]), (name, "svf")
-        assert torch.equal(out["sweep"][2], out[name][2]), (name, "sweeps")
+        for name in out:
+            assert torch.equal(out["sweep"][0], out[name][0]), (name, stay, "pi")
+            assert torch.equal(out["sweep"][1], out[name][1]), (name, stay, "svf")
+            assert torch.equal(out["sweep"][2], out[name][2]), (name, stay, "sweeps")
 
 
 def test_dense_to_ell_device(dev):
