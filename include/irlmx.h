@@ -148,10 +148,16 @@ int irlmx_backward_maxent(const irlmx_mdp* mdp, const double* reward, const uint
  * numpy's OpenBLAS dgemv_t sums it on a Haswell-family x86-64 host (lane
  * accumulators by column % 4, fused multiply-adds, lane and block sums), then
  * er * dot, the sequential action sum and za / zs -- so the policy is
- * bit-identical to the reference's there (oracle/blas_order.c pins the order).
+ * bit-identical to the reference's there (oracle/blas_order.c pins the order,
+ * against np.dot up to S = 4096 with one BLAS thread).  The reference's own bits
+ * depend on its host: above S = 625 numpy's multi-threaded OpenBLAS moves some
+ * rows to other kernels, so this is the reference run with
+ * OPENBLAS_NUM_THREADS=1 there (any thread count up to 625 states).
  * No rescaling: it overflows to NaN where the reference does.
  *   exp_reward [B][S]  np.exp(reward) as the reference computes it (maxent.py:142)
  * Requires S <= 4096 and S % 4 in {0, 1} (every square grid); IRLMX_EINVAL otherwise.
+ * ELL models: each row's nonzero entries in ascending column order per action
+ * (irlmx_dense_to_ell's layout), checked on the device; IRLMX_EINVAL otherwise.
  */
 int irlmx_backward_maxent_numpy_order(const irlmx_mdp* mdp, const double* exp_reward,
                                       const uint8_t* terminal, double* p_action, int32_t* status,
@@ -214,7 +220,9 @@ int irlmx_value_iteration(const irlmx_mdp* mdp, const double* reward, double dis
  * transcendental function: its values and sweep counts are bit-identical to the
  * reference's there.  Soft VI's exp / log are the device's (numpy's SIMD exp /
  * log may differ in the last bit): its dot products, and with them the
- * mirror-symmetric ties of its policy, follow numpy.  No workspace.
+ * mirror-symmetric ties of its policy, follow numpy.  No workspace.  The same
+ * single-thread caveat above S = 625 and ELL slot-order check as
+ * irlmx_backward_maxent_numpy_order.
  * Requires S <= 4096 and S % 4 in {0, 1}; IRLMX_EINVAL otherwise.
  */
 int irlmx_soft_backward_numpy_order(const irlmx_mdp* mdp, const double* reward, const double* terminal_reward,
@@ -231,7 +239,8 @@ int irlmx_value_iteration_numpy_order(const irlmx_mdp* mdp, const double* reward
  * Writes plan[IRLMX_PLAN_LEN]:
  *   [0] shape (IRLMX_SHAPE_*)   [1] R rows per tile   [2] G ghost rows
  *   [3] C tiles per instance   [4] instances per launch   [5] states per lane
- *   [6] in-tile layout (0 per state, 1 pair rows, 2 column pairs, 3 column quads)
+ *   [6] in-tile layout (0 per state, 1 pair rows, 2 column pairs, 3 column quads,
+ *       4 column quads with compact weights: the backward at width 256)
  *   [7] threads per workgroup  [8] sequential launches   [9] LDS bytes
  * Cluster fields are 0 for the other shapes.  Depends on the current device.
  * A backward plan assumes rescale != 0 unless op carries IRLMX_PLAN_NO_RESCALE.

@@ -2776,6 +2776,50 @@ extern "C" int irlmx_backward_maxent(const irlmx_mdp* mdp, const double* reward,
   return e == hipSuccess ? 0 : hip_fail(e, "backward");
 }
 
+// np_row_dot sums an ELL row's entries in slot order, which is numpy's order
+// only when every action's nonzero entries sit in ascending column order
+// (irlmx_dense_to_ell's layout; unused slots, value 0, are exact no-ops
+// anywhere).  One thread per (table instance, row): *bad set on a violation.
+__global__ void np_ell_ascending_kernel(Model m, int* bad) {
+  const int s = blockIdx.x * blockDim.x + threadIdx.x;
+  const int b = blockIdx.y;
+  if (s >= m.S) return;
+  for (int a = 0; a < m.A; ++a) {
+    int last = -1;
+    for (int k = 0; k < m.K; ++k) {
+      if (row_val(m, b, a, k, s) == 0.0) continue;
+      const int c = m.row_idx[((size_t)b * m.K + k) * m.S + s];
+      if (c <= last) { atomicOr(bad, 1); return; }
+      last = c;
+    }
+  }
+}
+
+// The numpy-order row dots' precondition on an ELL model (above); other
+// layouts visit their entries in column order by construction.  Synchronises.
+static int np_check_ell_rows(const Model& m, const char* fn, hipStream_t st) {
+  if (m.stencil || m.dense) return 0;
+  int* flag = nullptr;
+  hipError_t e = hipMallocAsync((void**)&flag, sizeof(int), st);
+  if (e != hipSuccess) return hip_fail(e, "numpy-order ELL check");
+  int h = 0;
+  e = hipMemsetAsync(flag, 0, sizeof(int), st);
+  if (e == hipSuccess) {
+    hipLaunchKernelGGL(np_ell_ascending_kernel, dim3((m.S + 255) / 256, m.shared ? 1 : m.B), dim3(256), 0, st, m,
+                       flag);
+    e = hipMemcpyAsync(&h, flag, sizeof(int), hipMemcpyDeviceToHost, st);
+  }
+  (void)hipFreeAsync(flag, st);
+  if (e == hipSuccess) e = hipStreamSynchronize(st);
+  if (e != hipSuccess) return hip_fail(e, "numpy-order ELL check");
+  if (h) {
+    set_error("%s: an ELL row holds its nonzero entries out of ascending column order (numpy's order needs "
+              "irlmx_dense_to_ell's slot layout)", fn);
+    return IRLMX_EINVAL;
+  }
+  return 0;
+}
+
 extern "C" int irlmx_backward_maxent_numpy_order(const irlmx_mdp* mdp, const double* exp_reward,
                                                  const uint8_t* terminal, double* p_action, int32_t* status,
                                                  void* stream) {
@@ -2790,6 +2834,7 @@ extern "C" int irlmx_backward_maxent_numpy_order(const irlmx_mdp* mdp, const dou
     return IRLMX_EINVAL;
   }
   hipStream_t st = (hipStream_t)stream;
+  if (int rc = np_check_ell_rows(m, "backward_maxent_numpy_order", st)) return rc;
   NpArgs a{m, exp_reward, terminal, p_action, status};
   const bool cached = m.stencil && m.S <= kNpCachedMaxStates && m.A <= kNpCachedMaxActions;
   void (*fn)(NpArgs) = cached ? (m.S <= kNpCachedThreads ? bwd_numpy_order_cached_kernel<1>
@@ -2954,6 +2999,7 @@ static int bellman_numpy_order(const irlmx_mdp* mdp, const double* reward, const
     set_error("%s: numpy's order is restated for S <= %d with S %% 4 in {0, 1}, got S=%d", fn, kFusedMaxStates, m.S);
     return IRLMX_EINVAL;
   }
+  if (int rc = np_check_ell_rows(m, fn, (hipStream_t)stream)) return rc;
   SoftArgs a{m, reward, phi, discount, eps, (long long)max_iter, average, p_action, value, iterations, status};
   void (*k)(SoftArgs) = nullptr;
   const bool cached = m.stencil && m.S <= kNpCachedMaxStates && m.A <= kNpCachedMaxActions;

@@ -6,6 +6,8 @@ building blocks of the numpy drop-ins (``maxent``, ``solver``) and of the
 batched IRL driver (``irlmx.batch``).
 """
 
+import os
+
 import numpy as np
 import torch
 
@@ -108,6 +110,28 @@ def numpy_order_supported(mdp, op="backward"):
     if op == "forward" and mdp.layout == _lib.LAYOUT_ELL:
         ok = ok and mdp.k_col <= 32
     return ok
+
+
+def numpy_order_default(mdp, op="backward"):
+    """Whether the drop-ins (maxent.py, solver.py) run ``op`` in numpy's order:
+    one instance, a model the numpy-order kernels cover, and at most
+    IRLMX_NUMPY_ORDER_MAX states (default 1024, where the register-cached
+    kernels run; IRLMX_NUMPY_ORDER_FWD_MAX overrides it for the forward) or
+    IRLMX_NUMPY_ORDER_DENSE_MAX on the DENSE layout (default 64).  Beyond, the
+    one-workgroup kernels re-read their entries every sweep: measured on one
+    MI355X (tools/diag/np_bwd_cost.py), the backward takes 31-435x the tiled
+    shapes' time at 33x33-64x64 (1.26 s vs 2.9 ms at 64x64) and 132x / 1,650x on
+    dense tables of 256 / 1024 states, soft VI 4-16x and 75-950x.  Above the caps
+    the drop-ins take the tiled shapes (within 1e-9 of the oracle; argmax ties may
+    fall differently).  IRLMX_NUMPY_ORDER=0 turns numpy's order off entirely."""
+    if mdp.batch != 1 or not numpy_order_supported(mdp, op) or os.environ.get("IRLMX_NUMPY_ORDER", "1") == "0":
+        return False
+    cap = int(os.environ.get("IRLMX_NUMPY_ORDER_MAX", "1024"))
+    if op == "forward":
+        cap = int(os.environ.get("IRLMX_NUMPY_ORDER_FWD_MAX", cap))
+    if mdp.layout == _lib.LAYOUT_DENSE:
+        cap = min(cap, int(os.environ.get("IRLMX_NUMPY_ORDER_DENSE_MAX", "64")))
+    return mdp.n_states <= cap
 
 
 def backward_maxent_numpy_order(mdp, exp_reward, terminal):
@@ -263,5 +287,5 @@ def stochastic_policy(successor, weighted_value):
     return out
 
 
-__all__ = ["DeviceMDP", "execution_plan", "counters", "terminal_mask", "backward_maxent", "forward_svf", "soft_backward",
+__all__ = ["DeviceMDP", "execution_plan", "numpy_order_default", "counters", "terminal_mask", "backward_maxent", "forward_svf", "soft_backward",
            "value_iteration", "dense_gemm", "dense_gemm_variant", "optimal_policy", "stochastic_policy"]

@@ -8,11 +8,15 @@ the feature products and the user's optimizer stay on the host, as in the
 reference's outer loop.
 
 The backward passes run in numpy's own floating-point order when the model
-allows it (S <= 4096 and S % 4 in {0, 1}: every square grid): the non-causal
+allows it (S % 4 in {0, 1}: every square grid; up to 1024 states by default,
+64 on a DENSE table, 4096 at most -- ops.numpy_order_default): the non-causal
 policy (local_action_probabilities, and the backward half of
 compute_expected_svf / irl) is then bit-identical to the reference's on a
 Haswell-family OpenBLAS host, and the soft VI's dot products follow numpy's
 order (ops.*_numpy_order; IRLMX_NUMPY_ORDER=0 turns it off).
+Above 625 states that is the reference run with one BLAS thread
+(OPENBLAS_NUM_THREADS=1): numpy's multi-threaded OpenBLAS partitions the rows
+differently there and its own last bits move with the thread count.
 
 Deliberate differences (documented in DESIGN.md):
 * Where the reference's backward pass overflows to NaN (about 13x13 at unit
@@ -104,14 +108,11 @@ def expected_svf_from_policy(p_transition, p_initial, terminal, p_action, eps=1e
 
 
 def _np_order(mdp, op="backward"):
-    """numpy's own summation order for this call (one instance, a model the
-    numpy-order kernels cover; IRLMX_NUMPY_ORDER=0 turns it off).  The forward
-    runs in numpy's order up to 1024 states (IRLMX_NUMPY_ORDER_FWD_MAX): its
-    one-workgroup kernel is slower per sweep than the tiled shapes, and larger
-    worlds run 10^5-10^6 sweeps (where the reference itself takes hours)."""
-    if mdp.batch != 1 or not ops.numpy_order_supported(mdp, op) or os.environ.get("IRLMX_NUMPY_ORDER", "1") == "0":
-        return False
-    return op != "forward" or mdp.n_states <= int(os.environ.get("IRLMX_NUMPY_ORDER_FWD_MAX", "1024"))
+    """numpy's own summation order for this call: one instance of a model the
+    numpy-order kernels cover, up to 1024 states (64 on a DENSE table) by
+    default -- ops.numpy_order_default states the caps, their measured cost and
+    the environment overrides (IRLMX_NUMPY_ORDER=0 turns it off)."""
+    return ops.numpy_order_default(mdp, op)
 
 
 def _forward(mdp, p_initial, term, pi, eps):

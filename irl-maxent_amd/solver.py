@@ -1,12 +1,13 @@
 """MI355X drop-in for the reference module ``solver`` (narendasan/irl-maxent, src/solver.py).
 
 Value iteration runs as a device fixed-point loop (irlmx.ops.value_iteration),
-in numpy's summation order where the model allows it (bit-identical values);
+in numpy's summation order where the model allows it (bit-identical values;
+above 625 states to the reference run with OPENBLAS_NUM_THREADS=1, whose
+multi-threaded row partition moves its own last bits);
 policy extraction gathers the intended successors' values on the device.
 Names, signatures, defaults and float64 numpy results follow the reference.
 """
 
-import os
 
 import numpy as np
 import torch
@@ -23,8 +24,9 @@ def _model(p):
 
 def _np_order(mdp):
     # numpy's summation order where the kernels cover the model: values bit-identical
-    # to the reference's (ops.value_iteration numpy_order; IRLMX_NUMPY_ORDER=0 turns it off)
-    return mdp.batch == 1 and ops.numpy_order_supported(mdp) and os.environ.get("IRLMX_NUMPY_ORDER", "1") != "0"
+    # to the reference's (ops.value_iteration numpy_order; caps and IRLMX_NUMPY_ORDER:
+    # ops.numpy_order_default)
+    return ops.numpy_order_default(mdp, "value_iteration")
 
 
 def value_iteration(p, reward, discount, eps=1e-3):

@@ -353,7 +353,7 @@ def test_backward_numpy_order_cached_against_restatement(dev, size):
     assert np.array_equal(pi[0].cpu().numpy(), ref)
 
 
-def test_backward_numpy_order_64x64_against_restatement(dev):
+def test_backward_numpy_order_64x64_against_restatement(dev, monkeypatch):
     """64x64 (S = 4096, the largest model the drop-ins run in numpy's order):
     the device's numpy-order backward against the C restatement of numpy's
     order (its sparse form, oracle/blas_order.c, pinned to the dense form and to
@@ -371,6 +371,9 @@ def test_backward_numpy_order_64x64_against_restatement(dev):
     mdp = DeviceMDP.icy_gridworld(size, 0.2, device=dev)
     pi = ops.backward_maxent_numpy_order(mdp, np.exp(r), ops.terminal_mask([n - 1], n, device=dev))
     assert np.array_equal(pi[0].cpu().numpy(), ref), np.max(np.abs(pi[0].cpu().numpy() - ref))
+    # (the drop-in's default numpy-order scope is 1024 states, ops.numpy_order_default)
+    assert not ops.numpy_order_default(mdp)
+    monkeypatch.setenv("IRLMX_NUMPY_ORDER_MAX", "4096")
     got = M.local_action_probabilities(O.icy_gridworld_table(size, 0.2), [n - 1], r)
     assert np.array_equal(got, ref)
     assert np.array_equal(np.argmax(got, axis=1), np.argmax(ref, axis=1))

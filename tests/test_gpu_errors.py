@@ -116,3 +116,28 @@ def test_counters_record_persistent_launches(world):
     c1 = ops.counters()
     assert c1["cluster_launches"] - c0["cluster_launches"] == 2
     assert c1["sweep_calls"] == c0["sweep_calls"] and c1["rerun_not_resident"] == c0["rerun_not_resident"]
+
+
+def test_numpy_order_rejects_unsorted_ell_rows(dev):
+    """The numpy-order entry points sum an ELL row's entries in slot order, which
+    is numpy's only for ascending columns (irlmx_dense_to_ell's layout): a model
+    whose row slots are reversed is refused with IRLMX_EINVAL and the message,
+    the sorted one runs (bit-identical to the oracle's restatement)."""
+    import maxent_oracle as O
+    from irlmx import DeviceMDP, ops
+    size = 5
+    S = size * size
+    P = O.icy_gridworld_table(size, 0.2)
+    good = DeviceMDP.from_dense(P, device=dev, layout="ell")
+    r = np.random.default_rng(1).uniform(0.0, 1.0, S)
+    tm = ops.terminal_mask([S - 1], S, device=dev)
+    pi = ops.backward_maxent_numpy_order(good, np.exp(r), tm)
+    assert np.array_equal(pi[0].cpu().numpy(), O.backward_maxent_blas_order(P, [S - 1], r))
+    rev = DeviceMDP(good.layout, S, good.n_actions, 1, good.shared, good.row_val.flip(-2).contiguous(),
+                    row_idx=good.row_idx.flip(-2).contiguous(), col_idx=good.col_idx, col_val=good.col_val,
+                    k_row=good.k_row, k_col=good.k_col, device=dev)
+    for call in (lambda: ops.backward_maxent_numpy_order(rev, np.exp(r), tm),
+                 lambda: ops.soft_backward(rev, r, O.terminal_reward([S - 1], S), 0.7, numpy_order=True),
+                 lambda: ops.value_iteration(rev, r, 0.9, numpy_order=True)):
+        with pytest.raises(Exception, match="ascending column order"):
+            call()
