@@ -767,7 +767,16 @@ __global__ void __launch_bounds__(NT) cluster_kernel(ClusterArgs a) {
 #pragma unroll
         for (int j = 0; j < (COLS ? SPT : 1); ++j) cv[j] = cw[j];
       }
-      __syncthreads();  // the last sweep's boundary reads are done
+#ifndef IRLMX_POST_SWEEP_BARRIER
+#define IRLMX_POST_SWEEP_BARRIER 0
+#endif
+      // CW: the band-edge array aliases the tile buffer the publication is
+      // staged in, so the last sweep's edge reads must be done first.  The other
+      // layouts' staging writes touch nothing a sweep reads (the tile buffer is
+      // read only between blocks, behind the barriers there), so their waves go
+      // on to the publication as they finish (IRLMX_POST_SWEEP_BARRIER=1: the r04
+      // barrier here, A/B)
+      if constexpr (CW || IRLMX_POST_SWEEP_BARRIER) __syncthreads();
     } else {
       run_sweeps(Tm, flags);
     }
