@@ -95,18 +95,26 @@ typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
 #endif
 constexpr int kGatherPerThread = 4;
 
-// Halo granule layout per instance: [2 parities][H rows][W + kGranRowPad] x 16 B,
-// parities and instances separated by a few more 128-B lines.  With the plain
-// [2][S] layout every tile's publication rows sat at power-of-two strides (rows
-// 4 KiB, tiles 64-128 KiB, parities and instances 256 KiB - 2 MiB apart), so
-// the publications of all tiles, both parities and all instances of an XCD
-// fell into the same few L2 sets: config 4 (width 256) wrote 274 GB of evicted
-// granule lines to HBM per backward launch, every store it made.  One extra
-// line per row and odd line offsets between parities and instances spread them
-// over the sets.
-constexpr int kGranRowPad = 8;                                    // granules (one 128-B line) per row
-__host__ __device__ inline size_t gran_par_len(int W, int H) { return (size_t)H * (W + kGranRowPad) + 24; }
-__host__ __device__ inline size_t gran_inst_len(int W, int H) { return 2 * gran_par_len(W, H) + 40; }
+// Halo granule layout per instance: [2 parities][S states (+ kGranRowPad per
+// row)] x 16 B, the parities and instances a few 128-B lines further apart than
+// their power-of-two sizes (24 and 40 granules).  Measured on one MI355X
+// (tools/diag/gran_layout_ab.sh): the config-4 backward's hand-off wait 3.1k ->
+// 2.5k cycles per block, 200 -> 192 ms per launch; config 3 unchanged (22.4-22.5
+// ms).  Padding every row as well (8 or 16 granules) gave the same times.
+#ifndef IRLMX_GRAN_ROW_PAD
+#define IRLMX_GRAN_ROW_PAD 0
+#endif
+#ifndef IRLMX_GRAN_PAR_PAD
+#define IRLMX_GRAN_PAR_PAD 24
+#endif
+#ifndef IRLMX_GRAN_INST_PAD
+#define IRLMX_GRAN_INST_PAD 40
+#endif
+constexpr int kGranRowPad = IRLMX_GRAN_ROW_PAD;                   // extra granules per row (8: one 128-B line)
+__host__ __device__ inline size_t gran_par_len(int W, int H) {
+  return (size_t)H * (W + kGranRowPad) + IRLMX_GRAN_PAR_PAD;
+}
+__host__ __device__ inline size_t gran_inst_len(int W, int H) { return 2 * gran_par_len(W, H) + IRLMX_GRAN_INST_PAD; }
 
 // A granule buffer: its descriptor (and, in IRLMX_DEVICE_CHECKS builds, its
 // byte length for the offset checks).

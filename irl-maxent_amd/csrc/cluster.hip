@@ -992,7 +992,15 @@ __global__ void __launch_bounds__(NT) cluster_kernel(ClusterArgs a) {
         if (MODE == kModeFwd) snap[l] = v;
       }
     }
-    __syncthreads();
+    // Column layouts (not CW) refresh only their own register slots from the
+    // tile buffer, and the next block's sweeps touch only registers and the
+    // band-edge array: a wave may start them while others still refresh (the
+    // next block's staging writes owned rows, its gather writes ghost rows only
+    // after the post-staging barrier).  Measured (tools/diag/ab_passes.py, three
+    // alternations on one box): one 128x128 instance's forward 14.53 -> 14.17 ms
+    // per 20,000 sweeps without this barrier, but config 3's backward 22.50 ->
+    // 22.77 ms -- so only the forward drops it.  (IRLMX_POST_SWEEP_BARRIER=1: as r04.)
+    if constexpr (!COLS || CW || MODE == kModeBwd || IRLMX_POST_SWEEP_BARRIER) __syncthreads();
     stamp(3);
     if (MODE == kModeBwd && done >= total) break;
   }
