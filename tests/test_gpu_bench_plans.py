@@ -334,3 +334,9 @@ def test_config3_whole_irl_run_against_oracle(dev):
         for k in keep:
             close(rec[b]["at"][k], z[f"{key}theta_at{k}"], (b, "theta", k))
         close(reward[b], z[key + "theta"], (b, "final reward"))
+        errs = {k: rel_err(rec[b]["at"][k], z[f"{key}theta_at{k}"]) for k in keep}
+        print(f"[whole run] instance {b}: {int(steps[b])} steps (oracle {int(z[key + 'steps'])}), "
+              f"forward sweeps identical at all {len(got_kf)} steps ({int(got_kf.sum())} in total), "
+              f"theta-sum max rel err {e:.2e}, theta rel err at steps " +
+              ", ".join(f"{k}: {v:.2e}" for k, v in errs.items()) +
+              f", final reward rel err {rel_err(reward[b], z[key + 'theta']):.2e}", flush=True)
