@@ -1013,6 +1013,12 @@ __global__ void __launch_bounds__(NT) cluster_kernel(ClusterArgs a) {
       for (int jp = 0; jp < SPT / 2; ++jp)
         if ((xb >> (2 * jp)) & 1u)
           *reinterpret_cast<double2*>(cur + pad + slot_state(2 * jp)) = make_double2(cv[PAIR ? 2 * jp : 0], cv[PAIR ? 2 * jp + 1 : 0]);
+      if constexpr (CW) {
+        // the pads and unused slots around the extended tile held band-edge rows
+        // (aliasing): back to 0, the value an off-grid neighbour reads below
+        for (int l = tid; l < pad; l += NT) cur[l] = 0.0;
+        for (int l = pad + E + tid; l < blen; l += NT) cur[l] = 0.0;
+      }
       __syncthreads();
     }
     // last of the 2*S sweeps, per action: za = exp(r) * (P_a zs); pi = za / sum_a za
