@@ -240,7 +240,9 @@ int irlmx_value_iteration_numpy_order(const irlmx_mdp* mdp, const double* reward
  *   [0] shape (IRLMX_SHAPE_*)   [1] R rows per tile   [2] G ghost rows
  *   [3] C tiles per instance   [4] instances per launch   [5] states per lane
  *   [6] in-tile layout (0 per state, 1 pair rows, 2 column pairs, 3 column quads,
- *       4 column quads with compact weights: the backward at width 256)
+ *       4 column quads with compact weights: the backward at width 256, for
+ *       tables that pass a device check of their structure -- so a width-256
+ *       STENCIL5 backward plan runs one small kernel and synchronises)
  *   [7] threads per workgroup  [8] sequential launches   [9] LDS bytes
  * Cluster fields are 0 for the other shapes.  Depends on the current device.
  * A backward plan assumes rescale != 0 unless op carries IRLMX_PLAN_NO_RESCALE.

@@ -465,14 +465,19 @@ __global__ void __launch_bounds__(NT) cluster_kernel(ClusterArgs a) {
 #ifndef IRLMX_FWD_BRANCH_ACCOUNT
 #define IRLMX_FWD_BRANCH_ACCOUNT 1
 #endif
+#ifndef IRLMX_FWD_BRANCH_SPT_MAX
+#define IRLMX_FWD_BRANCH_SPT_MAX 12
+#endif
       // With wave-uniform slot predicates (IRLMX_FWD_BRANCH_ACCOUNT): a scalar
       // branch per slot around the owned-delta update instead of computing it
       // for every slot and selecting -- the empty asm keeps the compiler from
       // speculating the body back into selects.  One 128² instance's forward
       // 0.736 -> 0.713 us per sweep, config 5 forward 127.0 -> 122.4 ms, same
-      // sweep counts.  (At 12 states per lane it spills 4-6 VGPRs: not used.)
+      // sweep counts.  Round 5: at 12 states per lane too (config 3's and the
+      // batched causal forward; two VGPRs spill, outside the sweep loop): B = 64
+      // at 128x128, 3,000 sweeps 3.19 -> 3.01 ms, three alternations on one box.
       auto account = [&](int j, double nv, double self) {
-        if constexpr (MODE == kModeFwd && kUniformSlots && SPT <= 8 && IRLMX_FWD_BRANCH_ACCOUNT) {
+        if constexpr (MODE == kModeFwd && kUniformSlots && SPT <= IRLMX_FWD_BRANCH_SPT_MAX && IRLMX_FWD_BRANCH_ACCOUNT) {
           if ((ob >> j) & 1u) {
             asm volatile("");
             dmax = fmax(dmax, fabs(nv - self));
