@@ -14,12 +14,8 @@ for path in glob.glob(os.path.join(src, "p*", "*counter_collection.csv")):
         if "cluster_kernel<1" not in r["Kernel_Name"]:
             continue
         vals[r["Counter_Name"]][int(r["Dispatch_Id"])] = float(r["Counter_Value"])
-last = {k: v[max(v)] for k, v in vals.items()}
-# (the counter passes sum per dispatch over all its instances; a dispatch's value is the sum)
-agg = {}
-for k, v in vals.items():
-    d = max(v)
-    agg[k] = sum(x for i, x in v.items() if i == d)
+# the last dispatch of the kernel in each pass (the driver's second, measured call)
+agg = {k: v[max(v)] for k, v in vals.items()}
 waves = agg.get("SQ_WAVES", 1.0)
 print(header)
 print("SQ_* cycle counters are quad-cycles (MI355X_MICROARCH.md); per wave-sweep = value / SQ_WAVES / sweeps.\n")

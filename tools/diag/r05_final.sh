@@ -8,6 +8,7 @@ tools/gpu_steps.sh \
   "r05_smoke|300|python -u -c 'import __graft_entry__ as g; g.smoke()'" \
   "r05_bench|400|python -u bench.py" \
   "r05_bench_c2|300|python -u bench.py --config c2 --steps 10 --warmup 3" \
+  "r05_bench_c2s|300|python -u bench.py --config c2s --steps 10 --warmup 3" \
   "r05_bench_c4|400|python -u bench.py --config c4 --steps 5 --warmup 2" \
   "r05_bench_c5|400|python -u bench.py --config c5 --steps 5 --warmup 2" \
   "r05_bench_c5b64|400|python -u bench.py --config c5 --batch 64 --steps 10 --warmup 3" \

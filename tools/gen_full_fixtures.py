@@ -14,12 +14,13 @@ irlmx.demos.sample with seed 1234 + b):
   full_c3.npz  128x128, B = 64: instances b = 0 and 63, the first 3 gradient
                steps of irl (maxent.py:240-252) from theta = 1 -- step 1's
                forward runs ~360k sweeps to convergence.
-  full_c4.npz  256x256, 32 instances per GPU: b = 0 and 31, the first 2 steps.
+  full_c4.npz  256x256, 32 instances per GPU: b = 0 and 31, the first 7 steps
+               (the bench's timed window at --steps 5 --warmup 2).
                Vectors of 65,536 states are stored on a fixed subset of 4,096
                states plus whole-vector sums (sum, sum |x|, max |x|).
   full_c5.npz  128x128 causal (config 5): the forward pass to convergence on the
                reference's own soft-VI policy (tests/golden/causal_128.npz), and
-               the first 2 irl_causal steps (maxent.py:437-450) of the bench's
+               the first 7 irl_causal steps (maxent.py:437-450) of the bench's
                c5 workload (one instance, discount 0.7).
 
   run_c3.npz   128x128, B = 64: instances b = 0 and 63 run to the reference's own
@@ -165,12 +166,12 @@ def main():
         jobs.append((job_dense, None))
     if "c3" in which:
         jobs += [(job_irl, ("c3", 128, 64, b, 3, False)) for b in (0, 63)]
-    if "c4" in which:
-        jobs += [(job_irl, ("c4", 256, 32, b, 2, False)) for b in (0, 31)]
+    if "c4" in which:   # 7 steps: the bench's --config c4 timed window (W = 2, K = 5) is steps 3-7
+        jobs += [(job_irl, ("c4", 256, 32, b, 7, False)) for b in (0, 31)]
     if "c3run" in which:
         jobs += [(job_run, ("c3", 128, 64, b)) for b in (0, 63)]
-    if "c5" in which:
-        jobs += [(job_c5_forward, None), (job_irl, ("c5", 128, 1, 0, 2, True))]
+    if "c5" in which:   # 7 steps, as config 4
+        jobs += [(job_c5_forward, None), (job_irl, ("c5", 128, 1, 0, 7, True))]
     with Pool(len(jobs)) as pool:
         res = [pool.apply_async(f, (a,)) for f, a in jobs]
         res = [r.get() for r in res]
