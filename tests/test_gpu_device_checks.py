@@ -4,7 +4,7 @@ built beside the product library by __graft_entry__.build()).
 One subprocess loads the check build (IRLMX_LIB) and runs the reference-pinned
 cases through every execution shape -- fused, per sweep, cluster with small
 tiles (halo exchanges, granule offsets, tile ranges), the persistent grid shape
-on an ELL model -- asserting the fixtures' results and no failed check; then a
+on an ELL model, the compact-weight column quads at width 256 -- asserting the fixtures' results and no failed check; then a
 model with a corrupted ELL index must raise the index bit instead of reading
 out of bounds.  (sanitizers run on the host build, see
 tests/test_host_sanitize.py; on the device this build is the bounds check.)
@@ -69,6 +69,20 @@ WORKER = textwrap.dedent("""
     p0 = np.zeros(n); p0[0] = 1.0
     ops.forward_svf(mdp, p0, tm, pi, max_iter=200)
     out["grid"] = ops.device_check_failures()
+    # width 256: the compact-weight column quads (cluster.hip LAY 4), the planner's
+    # plan and a forced one at 20 states per lane, against the per-sweep shape
+    size = 256; n = size * size
+    mdp = DeviceMDP.icy_gridworld(size, [0.15, 0.3], device=dev)
+    r = np.random.default_rng(8).uniform(-1.0, 1.0, (2, n))
+    tm = ops.terminal_mask([n - 1], n, batch=2, device=dev)
+    res = []
+    for env in ({{}}, {{"IRLMX_CLUSTER_R": "24", "IRLMX_CLUSTER_G": "8"}}, {{"IRLMX_CLUSTER": "0"}}):
+        for k in KEYS:
+            os.environ.pop(k, None)
+        os.environ.update(env)
+        res.append((ops.execution_plan(mdp, "backward")["layout"], ops.backward_maxent(mdp, r, tm)))
+    out["w256"] = [res[0][0], res[1][0], bool(torch.equal(res[0][1], res[2][1])),
+                   bool(torch.equal(res[1][1], res[2][1])), ops.device_check_failures()]
     # a corrupted ELL index: the check bit instead of an out-of-bounds read
     use("sweep")
     g = load_golden("generic")
@@ -96,5 +110,6 @@ def test_device_check_build(tmp_path):
         assert fails == 0, (shape, case, layout, fails)
         assert e_pi <= 1e-9 and e_svf <= 1e-8 and same_k, (shape, case, layout, e_pi, e_svf, same_k)
     assert out["grid"] == 0
+    assert out["w256"] == [4, 4, True, True, 0], out["w256"]
     assert out["corrupt"] & 1, out["corrupt"]   # kCheckIndex
     assert out["after"] == 0                    # cleared by the read
