@@ -43,3 +43,31 @@ def unpack_trajectories(flat, lens):
 @pytest.fixture(scope="session")
 def golden():
     return load_golden
+
+
+def icy_stencil_rect(W, H, p_slip):
+    """STENCIL5 row form [A = 4, 5, S] of an IcyGridWorld on a W x H grid: the
+    square builder's per-state rules (gridworld.py:177-248) with separate
+    widths and heights (no reference counterpart: the reference's worlds are
+    square; used to exercise rectangular tilings)."""
+    S = W * H
+    s = np.arange(S)
+    x, y = s % W, s // W
+    na = 4
+    p_int, p_nb = 1.0 - p_slip + p_slip / na, p_slip / na
+    corner = ((x == 0) | (x == W - 1)) & ((y == 0) | (y == H - 1))
+    edge = (x == 0) | (x == W - 1) | (y == 0) | (y == H - 1)
+    dirs = [(1, 0), (-1, 0), (0, 1), (0, -1)]            # actions (gridworld.py:47), also slots 1..4
+    rv = np.zeros((na, 5, S))
+    for a, (ax, ay) in enumerate(dirs):
+        for k, (dx, dy) in enumerate(dirs):
+            ok = (x + dx >= 0) & (x + dx < W) & (y + dy >= 0) & (y + dy < H)
+            rv[a, k + 1] = np.where(ok, p_int if (dx, dy) == (ax, ay) else p_nb, 0.0)
+        over = ~((x + ax >= 0) & (x + ax < W) & (y + ay >= 0) & (y + ay < H))
+        stay = np.zeros(S)
+        stay[over & corner] = 1.0 - p_slip + 2.0 * p_slip / na
+        stay[over & ~corner] = 1.0 - p_slip + p_slip / na
+        stay[~over & corner] = 2.0 * p_slip / na
+        stay[~over & ~corner & edge] = p_slip / na
+        rv[a, 0] = stay
+    return rv

@@ -21,7 +21,7 @@ import numpy as np
 import pytest
 
 import maxent_oracle as O
-from conftest import load_golden, unpack_trajectories
+from conftest import icy_stencil_rect, load_golden, unpack_trajectories
 
 pytestmark = pytest.mark.gpu
 
@@ -837,35 +837,6 @@ def test_deferred_convergence_caps_and_nan(dev, monkeypatch):
             assert int(a[3][3][1]) == 1 and int(a[4][2][1]) == 1  # IRLMX_NONFINITE for the inf-reward instance
 
 
-
-def _icy_stencil_rect(W, H, p_slip):
-    """STENCIL5 row form [A = 4, 5, S] of an IcyGridWorld on a W x H grid: the
-    square builder's per-state rules (gridworld.py:177-248) with separate
-    widths and heights (no reference counterpart: the reference's worlds are
-    square; used to exercise rectangular tilings)."""
-    S = W * H
-    s = np.arange(S)
-    x, y = s % W, s // W
-    na = 4
-    p_int, p_nb = 1.0 - p_slip + p_slip / na, p_slip / na
-    corner = ((x == 0) | (x == W - 1)) & ((y == 0) | (y == H - 1))
-    edge = (x == 0) | (x == W - 1) | (y == 0) | (y == H - 1)
-    dirs = [(1, 0), (-1, 0), (0, 1), (0, -1)]            # actions (gridworld.py:47), also slots 1..4
-    rv = np.zeros((na, 5, S))
-    for a, (ax, ay) in enumerate(dirs):
-        for k, (dx, dy) in enumerate(dirs):
-            ok = (x + dx >= 0) & (x + dx < W) & (y + dy >= 0) & (y + dy < H)
-            rv[a, k + 1] = np.where(ok, p_int if (dx, dy) == (ax, ay) else p_nb, 0.0)
-        over = ~((x + ax >= 0) & (x + ax < W) & (y + ay >= 0) & (y + ay < H))
-        stay = np.zeros(S)
-        stay[over & corner] = 1.0 - p_slip + 2.0 * p_slip / na
-        stay[over & ~corner] = 1.0 - p_slip + p_slip / na
-        stay[~over & corner] = 2.0 * p_slip / na
-        stay[~over & ~corner & edge] = p_slip / na
-        rv[a, 0] = stay
-    return rv
-
-
 @pytest.mark.parametrize("H,B", [(24, 1), (100, 3), (256, 33)])
 def test_compact_weights_rectangular_and_multi_launch(dev, monkeypatch, H, B):
     """The compact-weight backward (cluster.hip LAY 4) at width 256 on grids of
@@ -876,7 +847,7 @@ def test_compact_weights_rectangular_and_multi_launch(dev, monkeypatch, H, B):
     W = 256
     S = W * H
     slips = np.linspace(0.1, 0.3, B)
-    rv = np.stack([_icy_stencil_rect(W, H, p) for p in slips])
+    rv = np.stack([icy_stencil_rect(W, H, p) for p in slips])
     mdp = DeviceMDP(_lib.LAYOUT_STENCIL5, S, 4, B, False, torch.as_tensor(rv, device=dev), width=W, height=H,
                     device=dev)
     r = np.random.default_rng(H + B).uniform(-1.0, 1.0, (B, S))

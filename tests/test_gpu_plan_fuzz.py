@@ -1,0 +1,104 @@
+"""Seeded random tile plans of the cluster kernels against the per-sweep shape.
+
+The parity tests pin the planner's own plans and a few forced small ones; this
+draws 32 cases from a fixed seed -- grid width and height (square and
+rectangular, widths with compile-time LDS offsets and generic ones), batch,
+in-tile layout (IRLMX_PAIR), forced owned rows R and ghost rows G (ghosts wider
+than tiles included), rewards of both signs, terminals, initial distributions
+and forward caps -- and requires the cluster shape's policy, SVF, sweep counts
+and status to equal the per-sweep shape's bit for bit (both compute the same
+float64 operations in the same order: cluster.hip).  Cases whose forced plan
+does not fit a CU fall back to the planner's own plan (still compared); at
+least half of the (case, pass) pairs must run the forced cluster plan.
+"""
+
+import numpy as np
+import pytest
+
+from conftest import icy_stencil_rect
+
+pytestmark = pytest.mark.gpu
+
+torch = pytest.importorskip("torch")
+
+N_CASES = 32
+KEYS = ("IRLMX_FUSED_MAX_STATES", "IRLMX_CLUSTER", "IRLMX_CLUSTER_R", "IRLMX_CLUSTER_G", "IRLMX_PAIR",
+        "IRLMX_GRID", "IRLMX_COMPACT")
+
+
+@pytest.fixture(scope="module")
+def dev():
+    import __graft_entry__ as g
+    g.build()
+    import irlmx
+    return irlmx.require_device()
+
+
+def draw(rng):
+    W = int(rng.choice([16, 24, 37, 64, 128, 256]))
+    H = int(W if rng.random() < 0.5 else rng.integers(4, max(5, min(2 * W, 65536 // W))))
+    B = int(rng.integers(1, 5))
+    layouts = {64: [-1, 0, 1, 2], 128: [-1, 0, 1, 2, 3], 256: [-1, 0, 3, 4]}.get(W, [-1])
+    # rows one CU's registers hold at the smallest states-per-lane budget of the
+    # width's layouts (cluster.hip cluster_plan): forced plans mostly fit
+    rows = {64: 96, 128: 48, 256: 24}.get(W, 6144 // W)
+    G = int(rng.integers(1, min(16, max(1, rows // 2 - 1)) + 1))
+    R = int(rng.integers(1, max(1, min(H, rows - 2 * G)) + 1))
+    return dict(W=W, H=H, B=B, layout=int(rng.choice(layouts)), R=R, G=G,
+                # (random rewards can keep the forward from converging for
+                # millions of sweeps: every case has a cap)
+                cap=int(rng.choice([1, 7, 500, 3000, 20000])) if W * H > 4096 else 50000,
+                neg=bool(rng.random() < 0.5), seed=int(rng.integers(1 << 30)))
+
+
+def set_env(monkeypatch, env):
+    for k in KEYS:
+        monkeypatch.delenv(k, raising=False)
+    for k, v in env.items():
+        monkeypatch.setenv(k, str(v))
+
+
+def test_random_cluster_plans_bit_identical(dev, monkeypatch):
+    from irlmx import DeviceMDP, _lib, ops
+    rng = np.random.default_rng(20261018)
+    forced = 0
+    for i in range(N_CASES):
+        c = draw(rng)
+        W, H, B = c["W"], c["H"], c["B"]
+        S = W * H
+        r_ = np.random.default_rng(c["seed"])
+        slips = r_.uniform(0.05, 0.4, B)
+        if W == H and r_.random() < 0.5:
+            mdp = DeviceMDP.icy_gridworld(W, slips, device=dev)
+        else:
+            rv = np.stack([icy_stencil_rect(W, H, p) for p in slips])
+            mdp = DeviceMDP(_lib.LAYOUT_STENCIL5, S, 4, B, False, torch.as_tensor(rv, device=dev), width=W,
+                            height=H, device=dev)
+        lo = -1.0 if c["neg"] else 0.0
+        reward = r_.uniform(lo, 1.5, (B, S))
+        terminal = sorted(set([S - 1] + [int(t) for t in r_.integers(0, S, int(r_.integers(0, 3)))]))
+        tm = ops.terminal_mask(terminal, S, batch=B, device=dev)
+        p0 = r_.random((B, S)) ** 8
+        p0 /= p0.sum(axis=1, keepdims=True)
+        env = {"IRLMX_FUSED_MAX_STATES": 0, "IRLMX_CLUSTER_R": c["R"], "IRLMX_CLUSTER_G": c["G"]}
+        if c["layout"] >= 0:
+            env["IRLMX_PAIR"] = c["layout"]
+        out = {}
+        for name, e in (("cluster", env), ("sweep", {"IRLMX_FUSED_MAX_STATES": 0, "IRLMX_CLUSTER": 0})):
+            set_env(monkeypatch, e)
+            plans = [ops.execution_plan(mdp, op) for op in ("backward", "forward")]
+            pi = ops.backward_maxent(mdp, reward, tm)
+            svf, k, st = ops.forward_svf(mdp, p0, tm, pi, max_iter=c["cap"])
+            out[name] = (plans, pi, svf, k, st)
+        set_env(monkeypatch, {})
+        plans = out["cluster"][0]
+        hit = [p["shape"] == "cluster" and p["R"] == c["R"] and p["G"] == c["G"] for p in plans]
+        forced += sum(hit)
+        print(f"[fuzz {i}] {c} plans {[(p['shape'], p['R'], p['G'], p['C'], p['spt'], p['layout']) for p in plans]} "
+              f"k_f {out['sweep'][3].tolist()}", flush=True)
+        a, b = out["sweep"], out["cluster"]
+        assert torch.equal(a[1], b[1]), (i, c, "pi")
+        assert torch.equal(a[3], b[3]) and torch.equal(a[4], b[4]), (i, c, a[3].tolist(), b[3].tolist())
+        fin = torch.isfinite(a[2])
+        assert torch.equal(fin, torch.isfinite(b[2])) and torch.equal(a[2][fin], b[2][fin]), (i, c, "svf")
+    assert forced >= 2 * N_CASES // 2, forced
