@@ -102,3 +102,44 @@ def test_random_cluster_plans_bit_identical(dev, monkeypatch):
         fin = torch.isfinite(a[2])
         assert torch.equal(fin, torch.isfinite(b[2])) and torch.equal(a[2][fin], b[2][fin]), (i, c, "svf")
     assert forced >= 2 * N_CASES // 2, forced
+
+
+def test_random_soft_vi_and_vi_bit_identical(dev, monkeypatch):
+    """Soft VI (maxent.py:326-338) and value iteration (solver.py:40-50, 95-100)
+    on 16 seeded random grids (square and rectangular, batch 1-5, discounts
+    0.5-0.95, rewards of both signs, extra terminals) through the shape the
+    library picks (fused, or the persistent grid shape above 4,096 states)
+    against the per-sweep shape: values, policies, sweep counts and status bit
+    for bit."""
+    from irlmx import DeviceMDP, _lib, ops
+    from irlmx.batch import terminal_reward
+    rng = np.random.default_rng(181026)
+    shapes = set()
+    for i in range(16):
+        W = int(rng.choice([16, 37, 64, 128, 200, 256]))
+        H = int(W if rng.random() < 0.5 else rng.integers(4, max(5, min(2 * W, 65536 // W))))
+        B, S = int(rng.integers(1, 6)), W * H
+        gamma = float(rng.choice([0.5, 0.7, 0.9, 0.95]))
+        slips = rng.uniform(0.05, 0.4, B)
+        rv = np.stack([icy_stencil_rect(W, H, p) for p in slips])
+        mdp = DeviceMDP(_lib.LAYOUT_STENCIL5, S, 4, B, False, torch.as_tensor(rv, device=dev), width=W, height=H,
+                        device=dev)
+        r = rng.uniform(-1.0 if rng.random() < 0.5 else 0.0, 1.5, (B, S))
+        phi = terminal_reward(sorted(set([S - 1] + [int(t) for t in rng.integers(0, S, 2)])), S, B, dev)
+        out = {}
+        for name, env in (("default", {}), ("sweep", {"IRLMX_FUSED_MAX_STATES": 0, "IRLMX_GRID": 0})):
+            set_env(monkeypatch, env)
+            shape = ops.execution_plan(mdp, "soft_backward")["shape"]
+            out[name] = (ops.soft_backward(mdp, r, phi, gamma, max_iter=20000), ops.value_iteration(mdp, r, gamma),
+                         ops.value_iteration(mdp, r, gamma, average=True))
+            if name == "default":
+                shapes.add(shape)
+                case_shape = shape
+        set_env(monkeypatch, {})
+        print(f"[fuzz vi {i}] W={W} H={H} B={B} gamma={gamma} shape={case_shape} "
+              f"k_soft={out['sweep'][0][2].tolist()} k_vi={out['sweep'][1][1].tolist()}", flush=True)
+        for got, ref in zip(out["default"], out["sweep"]):
+            for x, y in zip(got, ref):
+                assert torch.equal(x.view(torch.int64) if x.dtype == torch.float64 else x,
+                                   y.view(torch.int64) if y.dtype == torch.float64 else y), (i, W, H, B, gamma)
+    assert "grid" in shapes, shapes
