@@ -500,6 +500,12 @@ __global__ void __launch_bounds__(NT) cluster_kernel(ClusterArgs a) {
           u[q] = make_double2(src[SPT - CPL + 2 * q], src[SPT - CPL + 2 * q + 1]);
         }
       }
+#ifndef IRLMX_PIN_STORES
+#define IRLMX_PIN_STORES 0
+#endif
+      // (IRLMX_PIN_STORES: experiments -- issue the edge-row stores before the
+      // first interior rows' FMAs, which then hide the stores' completion)
+      if constexpr (IRLMX_PIN_STORES && CPL == 2) __builtin_amdgcn_sched_barrier(0);
       if (MODE == kModeFwd && i == 0) {
         // forward: the block-start state into the LDS snapshot (for a stop inside
         // the block), here rather than at the block boundary so that the stores
