@@ -501,11 +501,18 @@ __global__ void __launch_bounds__(NT) cluster_kernel(ClusterArgs a) {
         }
       }
 #ifndef IRLMX_PIN_STORES
-#define IRLMX_PIN_STORES 0
+#define IRLMX_PIN_STORES -1
 #endif
-      // (IRLMX_PIN_STORES: experiments -- issue the edge-row stores before the
-      // first interior rows' FMAs, which then hide the stores' completion)
-      if constexpr (IRLMX_PIN_STORES && CPL == 2) __builtin_amdgcn_sched_barrier(0);
+      // Column pairs: issue the band-edge stores before the first interior rows'
+      // FMAs, which then cover the stores' completion ahead of the barrier (the
+      // scheduler otherwise sinks the stores below most of those FMAs).  Faster
+      // for the backward at up to 8 states per lane -- config 2's solo backward
+      // 2.81 -> 2.56 ms, one 128x128 instance 17.16 -> 16.70 ms -- slower at 12
+      // (config 3: 22.51 -> 23.6 ms), neutral for the forward
+      // (profiles/r05_ab_pin_stores.txt).  IRLMX_PIN_STORES: -1 that rule, 0 never, 1 always.
+      constexpr bool kPinStores =
+          CPL == 2 && (IRLMX_PIN_STORES < 0 ? (MODE == kModeBwd && SPT <= 8) : IRLMX_PIN_STORES != 0);
+      if constexpr (kPinStores) __builtin_amdgcn_sched_barrier(0);
       if (MODE == kModeFwd && i == 0) {
         // forward: the block-start state into the LDS snapshot (for a stop inside
         // the block), here rather than at the block boundary so that the stores
