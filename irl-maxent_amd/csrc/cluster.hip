@@ -511,7 +511,7 @@ __global__ void __launch_bounds__(NT) cluster_kernel(ClusterArgs a) {
       // (config 3: 22.51 -> 23.6 ms), neutral for the forward
       // (profiles/r05_ab_pin_stores.txt).  IRLMX_PIN_STORES: -1 that rule, 0 never, 1 always.
       constexpr bool kPinStores =
-          CPL == 2 && (IRLMX_PIN_STORES < 0 ? (MODE == kModeBwd && SPT <= 8) : IRLMX_PIN_STORES != 0);
+          IRLMX_PIN_STORES < 0 ? (CPL == 2 && MODE == kModeBwd && SPT <= 8) : IRLMX_PIN_STORES != 0;
       if constexpr (kPinStores) __builtin_amdgcn_sched_barrier(0);
       if (MODE == kModeFwd && i == 0) {
         // forward: the block-start state into the LDS snapshot (for a stop inside
