@@ -640,8 +640,13 @@ __global__ void __launch_bounds__(NT) cluster_kernel(ClusterArgs a) {
 #ifndef IRLMX_KPRE
 #define IRLMX_KPRE -1
 #endif
-      // (IRLMX_KPRE >= 0: experiments, interior steps before the barrier)
-      constexpr int kPre = IRLMX_KPRE >= 0 ? (IRLMX_KPRE < n_int ? IRLMX_KPRE : n_int) : (n_int + 1) / 2;
+      // (IRLMX_KPRE >= 0: experiments, interior steps before the barrier.)  The
+      // compact-weight quads run all their interior rows before the barrier:
+      // config 4's backward 193.3 / 189.8 -> 186.5 / 183.8 ms (two alternations;
+      // config 3's column pairs are slower that way, 22.50 -> 22.54-22.64 ms,
+      // profiles/r05_ab_c4_sched.txt)
+      constexpr int kPre = IRLMX_KPRE >= 0 ? (IRLMX_KPRE < n_int ? IRLMX_KPRE : n_int)
+                                           : (CW ? n_int : (n_int + 1) / 2);
       // IRLMX_QUAD_LAZY_ABOVE (quads): the row below is read at the barrier, the
       // row above only before the band's top row, so the two edge rows are never
       // live together (four doubles less register pressure; the hot loop has no

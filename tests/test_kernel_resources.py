@@ -4,7 +4,8 @@ kernel-resource-usage remarks for every instantiation of csrc/cluster.hip
 (tools/kernel_resources.py); CPU only (hipcc cross-compiles gfx950).
 
 Three instantiations may spill a few VGPRs: config 4's backward,
-cluster_kernel<1, 20, 256, 4, 512> (compact weights, 20 states per lane),
+cluster_kernel<1, 20, 256, 4, 512> (compact weights, 20 states per lane: 255
+VGPRs and no spill since round 5's schedule change, at the limit),
 config 3's forward, cluster_kernel<0, 12, 128, 2, 512> (owned-delta bookkeeping
 as scalar branches), and the same forward in column quads at width 256 (only
 planned when forced), all at 256 VGPRs.  Their spills must stay out of the
