@@ -510,8 +510,14 @@ __global__ void __launch_bounds__(NT) cluster_kernel(ClusterArgs a) {
       // 2.81 -> 2.56 ms, one 128x128 instance 17.16 -> 16.70 ms -- slower at 12
       // (config 3: 22.51 -> 23.6 ms), neutral for the forward
       // (profiles/r05_ab_pin_stores.txt).  IRLMX_PIN_STORES: -1 that rule, 0 never, 1 always.
+      // Config 3's backward (column pairs, 12 states per lane) is fastest with
+      // the store fence, both interior steps before the barrier and the barrier
+      // unpinned: 22.57 / 22.64 -> 22.24 / 22.23 ms (two alternations; at 8
+      // states per lane the same set is slower, config 2 2.57 -> 2.67 ms;
+      // profiles/r05_ab_c3_sched.txt)
+      constexpr bool kBwdPairs12 = CPL == 2 && MODE == kModeBwd && SPT >= 12;
       constexpr bool kPinStores =
-          IRLMX_PIN_STORES < 0 ? (CPL == 2 && MODE == kModeBwd && SPT <= 8) : IRLMX_PIN_STORES != 0;
+          IRLMX_PIN_STORES < 0 ? (CPL == 2 && MODE == kModeBwd && (SPT <= 8 || kBwdPairs12)) : IRLMX_PIN_STORES != 0;
       if constexpr (kPinStores) __builtin_amdgcn_sched_barrier(0);
       if (MODE == kModeFwd && i == 0) {
         // forward: the block-start state into the LDS snapshot (for a stop inside
@@ -540,7 +546,7 @@ __global__ void __launch_bounds__(NT) cluster_kernel(ClusterArgs a) {
       // loop body; config 3 backward 24.4 -> 23.0 ms on one box).  Column
       // quads are faster unpinned (267.6 vs 273.6 ms at config 4).
       // (IRLMX_PIN_BARRIER: -1 pairs only, 0 never, 1 always.)
-      constexpr bool kPin = IRLMX_PIN_BARRIER < 0 ? CPL == 2 : IRLMX_PIN_BARRIER != 0;
+      constexpr bool kPin = IRLMX_PIN_BARRIER < 0 ? (CPL == 2 && !kBwdPairs12) : IRLMX_PIN_BARRIER != 0;
       auto edges_in = [&](int which = 3, bool sync = true) {
         if (kPin && sync) __builtin_amdgcn_sched_barrier(0);
         if (sync) __syncthreads();
@@ -645,8 +651,14 @@ __global__ void __launch_bounds__(NT) cluster_kernel(ClusterArgs a) {
       // config 4's backward 193.3 / 189.8 -> 186.5 / 183.8 ms (two alternations;
       // config 3's column pairs are slower that way, 22.50 -> 22.54-22.64 ms,
       // profiles/r05_ab_c4_sched.txt)
+      // (config 3's backward: both interior steps, see kBwdPairs12; the
+      // forward in column pairs at <= 8 states per lane -- config 5's one
+      // instance, 6 per lane -- none: 14.25 / 14.30 -> 13.59 / 13.56 ms per
+      // 20,000 sweeps, but config 3's forward at 12 is slower that way)
       constexpr int kPre = IRLMX_KPRE >= 0 ? (IRLMX_KPRE < n_int ? IRLMX_KPRE : n_int)
-                                           : (CW ? n_int : (n_int + 1) / 2);
+                           : (CW || kBwdPairs12) ? n_int
+                           : (CPL == 2 && MODE == kModeFwd && SPT <= 8) ? 0
+                                                                       : (n_int + 1) / 2;
       // IRLMX_QUAD_LAZY_ABOVE (quads): the row below is read at the barrier, the
       // row above only before the band's top row, so the two edge rows are never
       // live together (four doubles less register pressure; the hot loop has no
