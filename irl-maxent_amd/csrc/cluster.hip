@@ -129,11 +129,16 @@ __global__ void __launch_bounds__(NT) cluster_kernel(ClusterArgs a) {
   constexpr int NB = COLS ? NT / HW : 1;                 // COLS: bands
   constexpr int QW = CPL / 2;                            // COLS: double2 per lane per row
 #ifndef IRLMX_LDS_SIDES
-#define IRLMX_LDS_SIDES 1
+#define IRLMX_LDS_SIDES -1
 #endif
   // COLS pairs: band edge rows' side neighbours from LDS (for quads, where 2 of
-  // 3 rows are edge rows, the exposed LDS latency costs more than the DPP moves)
-  constexpr bool kLdsSides = COLS && CPL == 2 && IRLMX_LDS_SIDES;
+  // 3 rows are edge rows, the exposed LDS latency costs more than the DPP moves).
+  // Forward only since round 5's backward schedule (store fence, unpinned
+  // barrier): DPP moves there are faster -- config 3's backward 22.09 / 22.13 ->
+  // 21.99 / 21.99 ms, config 2's 2.57 -> 2.40 ms -- while the forward keeps the
+  // LDS reads (one 128x128 instance 13.42 -> 13.82 ms per 20,000 sweeps with DPP;
+  // profiles/r05_ab_c3_sched.txt).  IRLMX_LDS_SIDES: -1 that rule, 0 never, 1 always.
+  constexpr bool kLdsSides = COLS && CPL == 2 && (IRLMX_LDS_SIDES < 0 ? MODE == kModeFwd : IRLMX_LDS_SIDES != 0);
 #ifndef IRLMX_COLS_RELOAD
 #define IRLMX_COLS_RELOAD 0
 #endif
