@@ -112,26 +112,51 @@ def numpy_order_supported(mdp, op="backward"):
     return ok
 
 
+# Default numpy-order scope of the drop-ins per op: (states on STENCIL5 / ELL
+# models, states on DENSE tables).  The kernels themselves cover 4096 states.
+NUMPY_ORDER_CAPS = {"backward": (1024, 64), "forward": (1024, 64),
+                    "soft_backward": (4096, 64), "value_iteration": (4096, 4096)}
+_CAP_ENV = {"backward": "BWD", "forward": "FWD", "soft_backward": "SOFT", "value_iteration": "VI"}
+
+
+def numpy_order_cap(mdp, op="backward"):
+    """The largest state count at which the drop-ins run ``op`` in numpy's order
+    on this model's layout (NUMPY_ORDER_CAPS; environment overrides: see
+    numpy_order_default)."""
+    sparse_cap, dense_cap = NUMPY_ORDER_CAPS[op]
+    cap = int(os.environ.get("IRLMX_NUMPY_ORDER_MAX", sparse_cap))
+    cap = int(os.environ.get(f"IRLMX_NUMPY_ORDER_{_CAP_ENV[op]}_MAX", cap))
+    if mdp.layout == _lib.LAYOUT_DENSE:
+        cap = min(cap, int(os.environ.get("IRLMX_NUMPY_ORDER_DENSE_MAX", dense_cap)))
+    return cap
+
+
 def numpy_order_default(mdp, op="backward"):
-    """Whether the drop-ins (maxent.py, solver.py) run ``op`` in numpy's order:
-    one instance, a model the numpy-order kernels cover, and at most
-    IRLMX_NUMPY_ORDER_MAX states (default 1024, where the register-cached
-    kernels run; IRLMX_NUMPY_ORDER_FWD_MAX overrides it for the forward) or
-    IRLMX_NUMPY_ORDER_DENSE_MAX on the DENSE layout (default 64).  Beyond, the
-    one-workgroup kernels re-read their entries every sweep: measured on one
-    MI355X (tools/diag/np_bwd_cost.py), the backward takes 31-435x the tiled
-    shapes' time at 33x33-64x64 (1.26 s vs 2.9 ms at 64x64) and 132x / 1,650x on
-    dense tables of 256 / 1024 states, soft VI 4-16x and 75-950x.  Above the caps
-    the drop-ins take the tiled shapes (within 1e-9 of the oracle; argmax ties may
-    fall differently).  IRLMX_NUMPY_ORDER=0 turns numpy's order off entirely."""
+    """Whether the drop-ins (maxent.py, solver.py) run ``op`` ("backward",
+    "forward", "soft_backward", "value_iteration") in numpy's order: one
+    instance, a model the numpy-order kernels cover, and at most
+    numpy_order_cap(mdp, op) states.
+
+    Caps per op (NUMPY_ORDER_CAPS): value iteration and soft VI run in numpy's
+    order on every model the kernels cover (4096 states; soft VI 64 on a DENSE
+    table), so solver.value_iteration / optimal_policy and
+    local_causal_action_probabilities reproduce the reference's values and argmax
+    at config 2's 64x64 (tests/golden/c2_64.npz).  The backward and the forward
+    stop at 1024 (64 on DENSE): beyond, their one-workgroup kernels re-read every
+    entry each of thousands of sweeps -- measured on one MI355X
+    (tools/diag/np_bwd_cost.py), the backward takes 31-435x the tiled shapes' time
+    at 33x33-64x64 (1.26 s vs 2.9 ms at 64x64) and 132x / 1,650x on dense tables of
+    256 / 1024 states; soft VI costs 4-16x on grids (milliseconds) but 75-950x on
+    dense tables, value iteration (tens of sweeps) stays in milliseconds to a
+    fraction of a second.  Above the caps the drop-ins take the tiled shapes
+    (within 1e-9 of the oracle; argmax ties may fall differently).
+
+    Environment: IRLMX_NUMPY_ORDER=0 turns numpy's order off;
+    IRLMX_NUMPY_ORDER_MAX sets every op's grid cap, IRLMX_NUMPY_ORDER_{BWD,FWD,
+    SOFT,VI}_MAX one op's, IRLMX_NUMPY_ORDER_DENSE_MAX the DENSE cap."""
     if mdp.batch != 1 or not numpy_order_supported(mdp, op) or os.environ.get("IRLMX_NUMPY_ORDER", "1") == "0":
         return False
-    cap = int(os.environ.get("IRLMX_NUMPY_ORDER_MAX", "1024"))
-    if op == "forward":
-        cap = int(os.environ.get("IRLMX_NUMPY_ORDER_FWD_MAX", cap))
-    if mdp.layout == _lib.LAYOUT_DENSE:
-        cap = min(cap, int(os.environ.get("IRLMX_NUMPY_ORDER_DENSE_MAX", "64")))
-    return mdp.n_states <= cap
+    return mdp.n_states <= numpy_order_cap(mdp, op)
 
 
 def backward_maxent_numpy_order(mdp, exp_reward, terminal):

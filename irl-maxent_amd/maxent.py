@@ -8,8 +8,9 @@ the feature products and the user's optimizer stay on the host, as in the
 reference's outer loop.
 
 The backward passes run in numpy's own floating-point order when the model
-allows it (S % 4 in {0, 1}: every square grid; up to 1024 states by default,
-64 on a DENSE table, 4096 at most -- ops.numpy_order_default): the non-causal
+allows it (S % 4 in {0, 1}: every square grid; by default up to 1024 states for
+the backward and forward, 4096 for soft VI, 64 on a DENSE table --
+ops.numpy_order_default): the non-causal
 policy (local_action_probabilities, and the backward half of
 compute_expected_svf / irl) is then bit-identical to the reference's on a
 Haswell-family OpenBLAS host, and the soft VI's dot products follow numpy's
@@ -109,9 +110,10 @@ def expected_svf_from_policy(p_transition, p_initial, terminal, p_action, eps=1e
 
 def _np_order(mdp, op="backward"):
     """numpy's own summation order for this call: one instance of a model the
-    numpy-order kernels cover, up to 1024 states (64 on a DENSE table) by
-    default -- ops.numpy_order_default states the caps, their measured cost and
-    the environment overrides (IRLMX_NUMPY_ORDER=0 turns it off)."""
+    numpy-order kernels cover, up to a per-op state count (backward / forward
+    1024, soft VI 4096; 64 on a DENSE table) -- ops.numpy_order_default states
+    the caps, their measured cost and the environment overrides
+    (IRLMX_NUMPY_ORDER=0 turns it off)."""
     return ops.numpy_order_default(mdp, op)
 
 
@@ -212,7 +214,7 @@ def local_causal_action_probabilities(p_transition, terminal, reward, discount, 
     """Soft value iteration of MaxCausalEnt IRL; returns exp(Q - V) (maxent.py:279-341)."""
     mdp = _model(p_transition)
     phi = _terminal_reward(terminal, mdp.n_states)
-    pi, _, _, _ = ops.soft_backward(mdp, reward, phi, discount, eps, numpy_order=_np_order(mdp))
+    pi, _, _, _ = ops.soft_backward(mdp, reward, phi, discount, eps, numpy_order=_np_order(mdp, "soft_backward"))
     return _host(pi)
 
 
@@ -221,7 +223,7 @@ def compute_expected_causal_svf(p_transition, p_initial, terminal, reward, disco
     """Soft value iteration then forward pass (maxent.py:344-380)."""
     mdp = _model(p_transition)
     phi = _terminal_reward(terminal, mdp.n_states)
-    pi, _, _, _ = ops.soft_backward(mdp, reward, phi, discount, eps_lap, numpy_order=_np_order(mdp))
+    pi, _, _, _ = ops.soft_backward(mdp, reward, phi, discount, eps_lap, numpy_order=_np_order(mdp, "soft_backward"))
     term = ops.terminal_mask(terminal, mdp.n_states, device=mdp.device)
     svf, _, _ = _forward(mdp, p_initial, term, pi, eps_svf)
     return _host(svf)
@@ -234,7 +236,7 @@ def irl_causal(p_transition, features, terminal, trajectories, optim, init, disc
     phi = torch.as_tensor(_terminal_reward(terminal, mdp.n_states), device=mdp.device)
 
     def svf_fn(m, reward, term, p0):
-        pi, _, _, _ = ops.soft_backward(m, reward, phi, discount, eps_lap, numpy_order=_np_order(m))
+        pi, _, _, _ = ops.soft_backward(m, reward, phi, discount, eps_lap, numpy_order=_np_order(m, "soft_backward"))
         svf, _, _ = _forward(m, p0, term, pi, eps_svf)
         return _host(svf)
 

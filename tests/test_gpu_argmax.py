@@ -377,3 +377,71 @@ def test_backward_numpy_order_64x64_against_restatement(dev, monkeypatch):
     got = M.local_action_probabilities(O.icy_gridworld_table(size, 0.2), [n - 1], r)
     assert np.array_equal(got, ref)
     assert np.array_equal(np.argmax(got, axis=1), np.argmax(ref, axis=1))
+
+
+class IcyWorld64:
+    """The reference IcyGridWorld(64, 0.2) API the solver drop-ins use: size,
+    actions, n_states / n_actions, state_index_transition, p_transition (the
+    oracle's table, sha256-equal to the reference builder's: tests/golden/c2_64.npz,
+    test_oracle_golden.py::test_c2_64_fixture_table)."""
+
+    def __init__(self):
+        self.size, self.n_states, self.n_actions = 64, 4096, 4
+        self.actions = O.ACTIONS
+        self.p_transition = O.icy_gridworld_table(64, 0.2)
+
+    def state_index_transition(self, s, a):
+        return O.intended_successor(self.size, s, a)
+
+
+def test_config2_drop_ins_against_reference(dev):
+    """BASELINE config 2's world (64x64 IcyGridWorld, A = 4, S = 4096) through the
+    drop-ins under their DEFAULT settings, against the reference run on the same
+    table with one BLAS thread (tests/golden/c2_64.npz, tools/gen_golden.py
+    c2_64): theta = 1 (mirror-symmetric exact ties, decided in the last bit) and
+    a seeded uniform theta.
+
+    * solver.value_iteration / stochastic_value_iteration (solver.py:9-104),
+      discounts 0.7 / 0.9: values bit-identical, sweep counts identical;
+      solver.optimal_policy_from_value and solver.optimal_policy
+      (solver.py:107-152): np.array_equal with the reference's greedy policy.
+    * maxent.local_causal_action_probabilities (maxent.py:279-341): argmax
+      identical at every state, ties included; policy within 1e-9 (exp / log
+      are the device's); soft-VI sweep count identical."""
+    import maxent as M
+    import solver as S
+    from irlmx import ops
+    z = load_golden("c2_64")
+    world = IcyWorld64()
+    P = world.p_transition
+    n = world.n_states
+    mdp = S._model(P)
+    assert ops.numpy_order_default(mdp, "value_iteration") and ops.numpy_order_default(mdp, "soft_backward")
+    names = [str(c) for c in z["names"]]
+    assert len(names) == 12
+    for c in names:
+        r = z[c.split("_")[0] + "__reward"]
+        g = float(z[c + "__discount"])
+        if "_soft_" in c:
+            ref = z[c + "__pi"]
+            pi = M.local_causal_action_probabilities(P, [n - 1], r, g)
+            got, want = np.argmax(pi, axis=1), np.argmax(ref, axis=1)
+            assert np.array_equal(got, want), (c, _argmax_report(got, want))
+            assert np.max(np.abs(pi - ref)) <= 1e-9 * np.max(np.abs(ref)), c
+            _, _, ks, st = ops.soft_backward(mdp, r, O.terminal_reward([n - 1], n), g, numpy_order=True)
+            assert int(ks[0]) == int(z[c + "__k_s"]) and int(st[0]) == 0, (c, int(ks[0]))
+            print(f"[c2_64] {c}: argmax equal at {n} states, {int(ks[0])} sweeps, "
+                  f"max |pi - ref| {np.max(np.abs(pi - ref)):.2e}", flush=True)
+            continue
+        avg = bool(z[c + "__average"])
+        fn = S.stochastic_value_iteration if avg else S.value_iteration
+        v = fn(P, r, g)
+        assert np.array_equal(v, z[c + "__value"]), (c, np.max(np.abs(v - z[c + "__value"])))
+        _, k, _ = ops.value_iteration(mdp, r, g, average=avg, numpy_order=True)
+        assert int(k[0]) == int(z[c + "__k"]), (c, int(k[0]))
+        pol = S.optimal_policy_from_value(world, v)
+        assert np.array_equal(pol, z[c + "__opt_policy"]), (c, _argmax_report(pol, z[c + "__opt_policy"]))
+        if not avg:
+            pol2 = S.optimal_policy(world, r, g)
+            assert np.array_equal(pol2, z[c + "__opt_policy"]), (c, _argmax_report(pol2, z[c + "__opt_policy"]))
+        print(f"[c2_64] {c}: values bit-identical, {int(k[0])} sweeps, greedy policy equal", flush=True)

@@ -280,28 +280,41 @@ def test_backward_lazy_summary_bit_identical(dev, monkeypatch, size, B):
     assert torch.equal(lazy, eager)
 
 
-def test_config3_whole_irl_run_against_oracle(dev):
-    """A whole config-3 ``irl`` run (maxent.py:236-255, eps = 1e-4) on the
-    benchmarked B = 64 plan, as ``bench.py``'s ``full_run`` does it
-    (BatchedMaxEnt.run with compaction), against the CPU oracle run to the
-    reference's own stopping rule for instances 0 and 63
-    (tests/golden/run_c3.npz, tools/gen_full_fixtures.py c3run, ~2.5 h each):
-    gradient-step count and every step's forward sweep count identical; theta
-    after steps 1, 2, 3, 6, 15, 25 (the bench's timed window at W = 5, K = 20)
-    and the final reward within 1e-9 relative (contract 1e-5); per-step
-    theta sums within 1e-9."""
+C2_BWD_PLAN = {"shape": "cluster", "R": 64, "G": 16, "C": 1, "per_launch": 1, "spt": 8, "layout": 2, "launches": 1}
+C2_FWD_PLAN = {"shape": "cluster", "R": 8, "G": 12, "C": 8, "per_launch": 1, "spt": 4, "layout": 2, "launches": 1}
+
+
+def test_config2_bench_plan_irl_steps(dev):
+    """Config 2 as bench.py --config c2 runs it (64x64, one instance, p_slip 0.1,
+    theta0 = 1): the solo backward plan (one tile holds the grid, R = 64, no
+    ghost rows: blocks of 256 sweeps) and the forward plan R = 8 / G = 12 /
+    C = 8 (ghost rows wider than tiles), asserted through irlmx_execution_plan;
+    the first 13 gradient steps (the recorded c2 bench's --warmup 3 --steps 10
+    window) against the CSR oracle's (tests/golden/full_c2.npz): forward sweep
+    counts identical, step 1's policy, every step's SVF and theta within 1e-9."""
+    from irlmx import ops
+    z, checked, mdp, steps = run_bench_workload(dev, "c2", 64, 1, fixture_steps("c2"))
+    assert plan_subset(ops.execution_plan(mdp, "backward"), C2_BWD_PLAN) == C2_BWD_PLAN
+    assert plan_subset(ops.execution_plan(mdp, "forward"), C2_FWD_PLAN) == C2_FWD_PLAN
+    compare_steps(z, checked, steps, 64 * 64)
+
+
+def whole_run_against_oracle(dev, cfg, size, B, bwd_plan):
+    """BatchedMaxEnt.run(compact=True) -- bench.py's full_run -- on the bench's
+    workload for `cfg` against tests/golden/run_<cfg>.npz (the CSR oracle's irl
+    loop to the reference's stopping rule for the checked instances)."""
     from irlmx import DeviceMDP, demos, ops
     from irlmx.batch import BatchedMaxEnt
     from irlmx.shard import instance_slips
     try:
-        z = load_golden("run_c3")
+        z = load_golden(f"run_{cfg}")
     except FileNotFoundError:
-        pytest.skip("tests/golden/run_c3.npz not generated")
-    size, B, S = 128, 64, 128 * 128
+        pytest.skip(f"tests/golden/run_{cfg}.npz not generated")
+    S = size * size
     checked = [int(b) for b in z["instances"]]
     slips = instance_slips(np.arange(B), B)
     mdp = DeviceMDP.icy_gridworld(size, slips, device=dev)
-    assert plan_subset(ops.execution_plan(mdp, "backward"), C3_BWD_PLAN) == C3_BWD_PLAN
+    assert plan_subset(ops.execution_plan(mdp, "backward"), bwd_plan) == bwd_plan
     rv = mdp.row_val.cpu().numpy()
     e_f = np.empty((B, S))
     p0 = np.empty((B, S))
@@ -344,8 +357,30 @@ def test_config3_whole_irl_run_against_oracle(dev):
             close(rec[b]["at"][k], z[f"{key}theta_at{k}"], (b, "theta", k))
         close(reward[b], z[key + "theta"], (b, "final reward"))
         errs = {k: rel_err(rec[b]["at"][k], z[f"{key}theta_at{k}"]) for k in keep}
-        print(f"[whole run] instance {b}: {int(steps[b])} steps (oracle {int(z[key + 'steps'])}), "
+        print(f"[whole run {cfg}] instance {b}: {int(steps[b])} steps (oracle {int(z[key + 'steps'])}), "
               f"forward sweeps identical at all {len(got_kf)} steps ({int(got_kf.sum())} in total), "
               f"theta-sum max rel err {e:.2e}, theta rel err at steps " +
               ", ".join(f"{k}: {v:.2e}" for k, v in errs.items()) +
               f", final reward rel err {rel_err(reward[b], z[key + 'theta']):.2e}", flush=True)
+
+
+def test_config3_whole_irl_run_against_oracle(dev):
+    """A whole config-3 ``irl`` run (maxent.py:236-255, eps = 1e-4) on the
+    benchmarked B = 64 plan, as ``bench.py``'s ``full_run`` does it
+    (BatchedMaxEnt.run with compaction), against the CPU oracle run to the
+    reference's own stopping rule for instances 0 and 63
+    (tests/golden/run_c3.npz, tools/gen_full_fixtures.py c3run, ~2.5 h each):
+    gradient-step count and every step's forward sweep count identical; theta
+    after steps 1, 2, 3, 6, 15, 25 (the bench's timed window at W = 5, K = 20)
+    and the final reward within 1e-9 relative (contract 1e-5); per-step
+    theta sums within 1e-9."""
+    whole_run_against_oracle(dev, "c3", 128, 64, C3_BWD_PLAN)
+
+
+def test_config2_whole_irl_run_against_oracle(dev):
+    """Config 2's whole ``irl`` run (64x64, one instance: the solo backward plan
+    and the R = 8 / G = 12 / C = 8 forward plan) against the CSR oracle run to the
+    reference's stopping rule (tests/golden/run_c2.npz, tools/gen_full_fixtures.py
+    c2run): step count and every step's forward sweep count identical, theta at
+    the kept steps and the final reward within 1e-9 relative."""
+    whole_run_against_oracle(dev, "c2", 64, 1, C2_BWD_PLAN)

@@ -214,7 +214,7 @@ def test_full_size_fixtures_consistent():
     workload matches the dense oracle's loop."""
     import numpy as np
     from irlmx import demos
-    for cfg, size, total in (("c3", 128, 64), ("c4", 256, 32), ("c5", 128, 1)):
+    for cfg, size, total in (("c2", 64, 1), ("c3", 128, 64), ("c4", 256, 32), ("c5", 128, 1)):
         z = load_golden(f"full_{cfg}")
         b = int(z["instances"][0])
         slip = 0.1 + 0.2 * b / total
@@ -247,6 +247,30 @@ def test_full_size_fixtures_consistent():
         theta = theta * np.exp(0.2 / (1 + k) * (e_f - svf))
         assert kf == res["k_f"][k]
         assert np.max(np.abs(theta - res["theta"][k])) <= 1e-12 * np.max(np.abs(theta))
+
+
+def test_c2_64_fixture_table():
+    """tests/golden/c2_64.npz (config 2's world through the reference, one BLAS
+    thread) was made on the reference builder's table, which equals the oracle's
+    64x64 IcyGridWorld byte for byte; value iteration in numpy's order restated
+    in C (oracle/blas_order.c) reproduces the reference's values and sweep counts
+    bit for bit at S = 4096 (both NBMAX = 2048 column blocks), and the CSR
+    restatement within 1e-12 with the same sweep counts."""
+    z = load_golden("c2_64")
+    assert int(z["size"]) == 64 and float(z["p_slip"]) == 0.2
+    P = O.icy_gridworld_table(64, 0.2)
+    assert hashlib.sha256(np.ascontiguousarray(P).tobytes()).hexdigest() == str(z["P_sha256"])
+    mats = O.icy_gridworld_csr(64, 0.2)
+    for c in ("ones_g7_max", "unif_g7_avg", "unif_g9_max"):
+        r = z[c.split("_")[0] + "__reward"]
+        g, avg = float(z[c + "__discount"]), bool(z[c + "__average"])
+        v, k = O.value_iteration_blas_order(P, r, g, average=avg)
+        assert k == int(z[c + "__k"]) and np.array_equal(v, z[c + "__value"]), c
+        vs, ks = O.value_iteration_csr(mats, r, g, average=avg)
+        assert ks == k and np.max(np.abs(vs - v)) <= 1e-12 * np.max(np.abs(v)), c
+    # the reference's greedy policy from its own values (solver.py:107-124)
+    for c in ("ones_g9_max", "unif_g7_max"):
+        assert np.array_equal(O.optimal_policy_from_value(64, z[c + "__value"]), z[c + "__opt_policy"]), c
 
 
 def test_demos_truncation_reported():

@@ -23,6 +23,13 @@ irlmx.demos.sample with seed 1234 + b):
                the first 7 irl_causal steps (maxent.py:437-450) of the bench's
                c5 workload (one instance, discount 0.7).
 
+  full_c2.npz  64x64, one instance (BASELINE config 2 as bench.py --config c2 runs
+               it: p_slip 0.1, demonstrations seed 1234): the first 13 steps
+               (the recorded c2 bench window, --warmup 3 --steps 10), full
+               policy of step 1, SVF and theta of every step.
+  run_c2.npz   the same instance run to the reference's stopping rule (as
+               run_c3.npz below; a few minutes).
+
   run_c3.npz   128x128, B = 64: instances b = 0 and 63 run to the reference's own
                stopping rule (maxent.py:236-255, eps = 1e-4) -- step count,
                per-step forward sweeps and theta summaries, theta after steps
@@ -36,7 +43,7 @@ irlmx.demos.sample with seed 1234 + b):
                backward, forward, soft VI + causal forward, VI and its
                action-average form, with sweep counts.
 
-Usage: python tools/gen_full_fixtures.py [c3 c4 c5 dense c3run]
+Usage: python tools/gen_full_fixtures.py [c2 c2run c3 c4 c5 dense c3run]
        (~25 min on 8 cores without c3run)
 """
 
@@ -107,7 +114,7 @@ def job_irl(args):
     return cfg, b, out
 
 
-RUN_KEEP = (1, 2, 3, 6, 15, 25)
+RUN_KEEP = (1, 2, 3, 6, 13, 15, 25)
 
 
 def job_run(args):
@@ -168,6 +175,10 @@ def main():
         jobs += [(job_irl, ("c3", 128, 64, b, 3, False)) for b in (0, 63)]
     if "c4" in which:   # 7 steps: the bench's --config c4 timed window (W = 2, K = 5) is steps 3-7
         jobs += [(job_irl, ("c4", 256, 32, b, 7, False)) for b in (0, 31)]
+    if "c2" in which:   # 13 steps: the recorded c2 bench window (W = 3, K = 10)
+        jobs.append((job_irl, ("c2", 64, 1, 0, 13, False)))
+    if "c2run" in which:
+        jobs.append((job_run, ("c2", 64, 1, 0)))
     if "c3run" in which:
         jobs += [(job_run, ("c3", 128, 64, b)) for b in (0, 63)]
     if "c5" in which:   # 7 steps, as config 4

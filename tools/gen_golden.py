@@ -395,9 +395,55 @@ def gen_optimizers():
     save("optimizers", **out)
 
 
+def gen_c2_64():
+    """G8 (heavy, ~0.6 GB RAM, a few minutes): BASELINE config 2's world, 64x64
+    IcyGridWorld (A = 4, p_slip 0.2, S = 4096), built by the reference's own
+    builder, run through the reference with ONE BLAS thread (above 625 states
+    numpy's multi-threaded row partition moves its own last bits, DESIGN.md
+    section 2): value_iteration and stochastic_value_iteration (solver.py:9-104)
+    at discounts 0.7 / 0.9 with values, sweep counts and optimal_policy_from_value
+    (solver.py:107-124); local_causal_action_probabilities (maxent.py:279-341)
+    with policy and sweep count.  Rewards: theta = 1 (mirror-symmetric states are
+    exact ties that the last bit decides) and a seeded uniform theta."""
+    from threadpoolctl import threadpool_limits
+    size, p_slip = 64, 0.2
+    n = size * size
+    t0 = time.time()
+    world = W.IcyGridWorld(size, p_slip)
+    P = world.p_transition
+    assert np.array_equal(P, ORC.icy_gridworld_table(size, p_slip))
+    print(f"c2_64: reference table built in {time.time() - t0:.0f}s")
+    rng = np.random.default_rng(64)
+    rewards = {"ones": np.ones(n), "unif": rng.uniform(0.0, 1.5, n)}
+    out = {"size": size, "p_slip": p_slip, "terminal": np.array([n - 1]),
+           "P_sha256": np.array(hashlib.sha256(np.ascontiguousarray(P).tobytes()).hexdigest())}
+    names = []
+    with threadpool_limits(limits=1, user_api="blas"):
+        for rname, r in rewards.items():
+            out[f"{rname}__reward"] = r
+            for gamma in (0.7, 0.9):
+                for avg in (False, True):
+                    name = f"{rname}_g{int(gamma * 10)}_{'avg' if avg else 'max'}"
+                    t0 = time.time()
+                    v, k = ref_vi(P, r, gamma, average=avg)
+                    out.update({f"{name}__discount": gamma, f"{name}__average": avg, f"{name}__value": v,
+                                f"{name}__k": k, f"{name}__opt_policy": S.optimal_policy_from_value(world, v)})
+                    names.append(name)
+                    print(f"c2_64 vi {name}: k={k} {time.time() - t0:.1f}s", flush=True)
+            for gamma in (0.7, 0.9):
+                name = f"{rname}_soft_g{int(gamma * 10)}"
+                t0 = time.time()
+                pi, k_s = ref_soft(P, [n - 1], r, gamma)
+                out.update({f"{name}__discount": gamma, f"{name}__pi": pi, f"{name}__k_s": k_s})
+                names.append(name)
+                print(f"c2_64 soft {name}: k_s={k_s} {time.time() - t0:.1f}s", flush=True)
+    out["names"] = np.array(names)
+    save("c2_64", **out)
+
+
 GENS = {"config1": gen_config1, "maxent_small": gen_maxent_small, "causal_small": gen_causal_small,
         "worlds": gen_worlds, "vi": gen_vi, "generic": gen_generic, "optimizers": gen_optimizers}
-HEAVY = {"causal_128": gen_causal_128}
+HEAVY = {"causal_128": gen_causal_128, "c2_64": gen_c2_64}
 
 
 def main():
