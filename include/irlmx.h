@@ -76,6 +76,9 @@ extern "C" {
  *    col_val[b'][s][t]    = sum_a P[s, t, a]  (action-summed, for the backward)
  *    row_idx, col_idx unused; k_row = k_col = n_states.
  *  b' = 0 when `shared` is nonzero (one table for all B instances), else b.
+ *  props: 0 (unknown: entry points that depend on a table property check it on
+ *  the device per call, which synchronises the stream) or the value
+ *  irlmx_mdp_properties() returned for exactly these table contents.
  */
 typedef struct irlmx_mdp {
   int32_t layout;
@@ -87,7 +90,7 @@ typedef struct irlmx_mdp {
   int32_t k_col;  /* slots per state in the column form (ELL) */
   int32_t batch;
   int32_t shared;
-  int32_t reserved;
+  int32_t props;  /* 0, or irlmx_mdp_properties()'s result for these tables (see there) */
   const double* row_val;
   const int32_t* row_idx;
   const int32_t* col_idx;
@@ -126,6 +129,25 @@ int irlmx_counters(int64_t* out, int32_t n);
 int irlmx_device_checks_enabled(void);
 int64_t irlmx_device_check_failures(void);
 
+/*
+ * Structural properties of the model's tables (no reference counterpart), so
+ * that calls need not re-check them: computed on the device once, written to
+ * *props (IRLMX_PROPS_KNOWN | the IRLMX_PROP_* bits that hold); synchronises
+ * `stream`.  Store the value in irlmx_mdp.props for later calls on the same
+ * tables; it describes their contents when computed -- edit a table in place and
+ * props must go back to 0 (or be recomputed).
+ *   IRLMX_PROP_COMPACT     STENCIL5: the collapsed backward coefficients have
+ *                          the structure of the compact-weight cluster layout
+ *                          (equal +x / -x coefficients inside the grid, no self
+ *                          coefficient off the border; used at width 256)
+ *   IRLMX_PROP_ELL_SORTED  ELL: every row holds its nonzero entries in ascending
+ *                          column order (the *_numpy_order entry points need it)
+ */
+#define IRLMX_PROPS_KNOWN 0x40000000
+#define IRLMX_PROP_COMPACT 0x1
+#define IRLMX_PROP_ELL_SORTED 0x2
+int irlmx_mdp_properties(const irlmx_mdp* mdp, int32_t* props, void* stream);
+
 /* Bytes of device workspace `op` needs for this model (0 is a valid answer). */
 size_t irlmx_workspace_bytes(const irlmx_mdp* mdp, int32_t op);
 
@@ -157,7 +179,8 @@ int irlmx_backward_maxent(const irlmx_mdp* mdp, const double* reward, const uint
  *   exp_reward [B][S]  np.exp(reward) as the reference computes it (maxent.py:142)
  * Requires S <= 4096 and S % 4 in {0, 1} (every square grid); IRLMX_EINVAL otherwise.
  * ELL models: each row's nonzero entries in ascending column order per action
- * (irlmx_dense_to_ell's layout), checked on the device; IRLMX_EINVAL otherwise.
+ * (irlmx_dense_to_ell's layout), checked on the device (or taken from props);
+ * IRLMX_EINVAL otherwise.
  */
 int irlmx_backward_maxent_numpy_order(const irlmx_mdp* mdp, const double* exp_reward,
                                       const uint8_t* terminal, double* p_action, int32_t* status,
@@ -241,8 +264,8 @@ int irlmx_value_iteration_numpy_order(const irlmx_mdp* mdp, const double* reward
  *   [3] C tiles per instance   [4] instances per launch   [5] states per lane
  *   [6] in-tile layout (0 per state, 1 pair rows, 2 column pairs, 3 column quads,
  *       4 column quads with compact weights: the backward at width 256, for
- *       tables that pass a device check of their structure -- so a width-256
- *       STENCIL5 backward plan runs one small kernel and synchronises)
+ *       tables with IRLMX_PROP_COMPACT -- without props, a width-256 STENCIL5
+ *       backward plan checks the table on the device and synchronises)
  *   [7] threads per workgroup  [8] sequential launches   [9] LDS bytes
  * Cluster fields are 0 for the other shapes.  Depends on the current device.
  * A backward plan assumes rescale != 0 unless op carries IRLMX_PLAN_NO_RESCALE.

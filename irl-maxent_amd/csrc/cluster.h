@@ -260,7 +260,8 @@ constexpr int kClusterNotResident = 2;
 // (bwd_compact_ok_kernel); the planner then considers it at width 256
 bool cluster_plan(int W, int H, int B, int mode, ClusterPlan* out, bool compact = false);
 int cluster_run(int mode, const ClusterPlan& p, ClusterArgs a, int B, hipStream_t st);
-__global__ void bwd_growth_kernel(const double* __restrict__ bw, int S, int B, unsigned long long* __restrict__ growth);
+__global__ void bwd_growth_kernel(const double* __restrict__ bw, int W, int S, int B,
+                                  unsigned long long* __restrict__ growth);
 __global__ void bwd_compact_ok_kernel(const double* __restrict__ row_val, int W, int H, int A, int* __restrict__ bad);
 
 }  // namespace irlmx

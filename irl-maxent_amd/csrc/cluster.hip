@@ -341,9 +341,10 @@ __global__ void __launch_bounds__(NT) cluster_kernel(ClusterArgs a) {
   // Backward rescaling period: blocks between rescales (see the block loop).
   // Between two rescales the partition vector neither grows nor shrinks by more
   // than 2^900: its maximum grows at most by g = max_s sum_k w_k(s) per sweep
-  // and shrinks at most by d = the smallest positive weight (every grid state is
-  // some in-grid neighbour's stencil target with a positive weight, so the state
-  // holding the maximum feeds at least d times it into the next sweep).  The
+  // and shrinks at most by d = the smallest positive weight (when every state is
+  // some state's stencil operand with a positive weight -- checked by
+  // bwd_growth_kernel -- the state holding the maximum feeds at least d times it
+  // into the next sweep; otherwise short blocks, rescaled every block).  The
   // sweeps between rescales, T * p_max, are capped at 900 / log2 of either rate
   // -- which shortens the solo backward's 256-sweep blocks (kSoloBwdT) where
   // the rewards are very negative (decay) or the growth is near 2 per sweep.
@@ -355,8 +356,11 @@ __global__ void __launch_bounds__(NT) cluster_kernel(ClusterArgs a) {
       int cap = 1 << 20;
       if (g > 1.0) cap = max(1, (int)floor(900.0 / log2(g)) - 1);
       if (d > 0.0 && d < 1.0) cap = min(cap, max(1, (int)floor(900.0 / -log2(d)) - 1));
+      // no decay bound (a state feeds nobody, bwd_growth_kernel): blocks of at
+      // most kTMax sweeps, rescaled every block (the round-3 cadence)
+      if (d < 0.0) cap = min(cap, kTMax);
       T = max(1, min(T, cap));
-      p_max = max(1, min(kRescaleEvery, cap / T));
+      p_max = d < 0.0 ? 1 : max(1, min(kRescaleEvery, cap / T));
     }
   }
   __syncthreads();
@@ -1093,11 +1097,20 @@ namespace irlmx {
 // Per-instance bounds on the backward's per-sweep growth and decay (reward-folded
 // weights, fixed_point.hip bwd_weights_kernel): growth[b] = max_s sum_k bw[b][k][s],
 // growth[B + b] = the smallest positive weight (both as float64 bits; the
-// weights are non-negative, so the bits order like the values).
-__global__ void bwd_growth_kernel(const double* __restrict__ bw, int S, int B, unsigned long long* __restrict__ growth) {
+// weights are non-negative, so the bits order like the values).  The decay bound
+// rests on every state feeding some state with a positive weight (its value is
+// a stencil operand of itself or of an in-grid neighbour): then the state holding
+// the maximum passes at least that weight times it into the next sweep.  A table
+// with a state that feeds nobody (its neighbours' weights towards it are all 0)
+// has no such bound: growth[B + b] = kNoDecayBound, and the kernel falls back to
+// short blocks rescaled every block (cluster_kernel, p_max).
+constexpr unsigned long long kNoDecayBound = 0xBFF0000000000000ull;  // bits of -1.0
+__global__ void bwd_growth_kernel(const double* __restrict__ bw, int W, int S, int B,
+                                  unsigned long long* __restrict__ growth) {
   const int b = blockIdx.x;
   const double* wb = bw + (size_t)b * kStencilK * S;
   unsigned long long mx = 0ull, mn = ~0ull;
+  unsigned dead = 0u;  // some state feeds no state with a positive weight
   for (int s = threadIdx.x; s < S; s += blockDim.x) {
     double row = 0.0;
     for (int k = 0; k < kStencilK; ++k) {
@@ -1106,8 +1119,19 @@ __global__ void bwd_growth_kernel(const double* __restrict__ bw, int S, int B, u
       if (x > 0.0) mn = min(mn, abs_bits(x));
     }
     mx = max(mx, abs_bits(row));
+    // s is slot k's neighbour of: itself (0), s - 1 (+x, 1), s + 1 (-x, 2), s - W (+y, 3), s + W (-y, 4)
+    const int x = s % W;
+    const bool feeds = wb[s] > 0.0 || (x > 0 && wb[(size_t)1 * S + s - 1] > 0.0) ||
+                       (x + 1 < W && wb[(size_t)2 * S + s + 1] > 0.0) ||
+                       (s >= W && wb[(size_t)3 * S + s - W] > 0.0) ||
+                       (s + W < S && wb[(size_t)4 * S + s + W] > 0.0);
+    dead |= feeds ? 0u : 1u;
   }
   __shared__ unsigned long long red[2][16];
+  __shared__ unsigned dead_l;
+  if (threadIdx.x == 0) dead_l = 0u;
+  __syncthreads();
+  if (dead) atomicOr(&dead_l, 1u);
   mx = wave_max_u64(mx);
   mn = ~wave_max_u64(~mn);
   if ((threadIdx.x & 63) == 0) { red[0][threadIdx.x / 64] = mx; red[1][threadIdx.x / 64] = mn; }
@@ -1115,7 +1139,8 @@ __global__ void bwd_growth_kernel(const double* __restrict__ bw, int S, int B, u
   if (threadIdx.x == 0) {
     for (int i = 1; i < (int)(blockDim.x / 64); ++i) { mx = max(mx, red[0][i]); mn = min(mn, red[1][i]); }
     growth[b] = mx;
-    growth[B + b] = mn == ~0ull ? 0ull : mn;  // no positive weight: no decay bound (0)
+    // no positive weight: no decay at all (0); a state that feeds nobody: no bound
+    growth[B + b] = dead_l ? kNoDecayBound : (mn == ~0ull ? 0ull : mn);
   }
 }
 

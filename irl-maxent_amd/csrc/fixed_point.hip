@@ -68,6 +68,7 @@ constexpr int kSweepThreads = 256;
 
 struct Model {
   int S, A, K, W, H, B, stencil, shared, Kc, dense;
+  int props;  // irlmx_mdp.props: IRLMX_PROPS_KNOWN | IRLMX_PROP_* from irlmx_mdp_properties, or 0 (unknown)
   const double* row_val;
   const int32_t* row_idx;
   const int32_t* col_idx;
@@ -90,6 +91,7 @@ static Model make_model(const irlmx_mdp* m) {
   o.row_idx = m->row_idx;
   o.col_idx = m->col_idx;
   o.col_val = m->col_val;
+  o.props = m->props;
   return o;
 }
 
@@ -126,11 +128,13 @@ struct Ws {
   int32_t* done;              // [B]
   int64_t* iters;             // [B]
   int32_t* ndone;             // [1]
-  // cluster shape (stencil layouts too large for one CU)
-  unsigned long long* gran;   // [B][2][S] x 16 B
-  unsigned long long* sgran;  // [B][3][H] x 16 B
-  unsigned long long* growth; // [2][B] growth / decay bounds
-  int* err;                   // [1]
+  // cluster shape (stencil layouts too large for one CU); sizes as carve() takes them:
+  unsigned long long* gran;   // cluster: [B][gran_inst_len(W, H)] x 16 B (two padded halo parities, cluster.h);
+                              // grid: [B][3][S] x 16 B; dense grid: [B][2][S] x 16 B
+  unsigned long long* sgran;  // cluster: [B][kSumSlots + 1][H] x 16 B (tile summaries by block % kSumSlots,
+                              // then the XCC ids); grid: [B][4][bpi]; dense grid: [B][bpi] x 16 B
+  unsigned long long* growth; // [2][B] growth / decay bounds (bwd_growth_kernel)
+  int* err;                   // [4]: error bits, rendezvous counters
   size_t total;
 };
 
@@ -2525,11 +2529,11 @@ extern "C" int irlmx_dense_to_rows(const double* dense, int32_t n_states, int32_
 
 namespace irlmx {
 // The backward's tables fit the compact-weight cluster layout (cluster.hip,
-// LAY 4: width 256 only)?  Checked on the device per call
-// (bwd_compact_ok_kernel), one int of device memory as the flag; synchronises
-// the stream.  IRLMX_COMPACT=0 turns the layout off.
-static bool bwd_compact(const Model& m, int* flag, hipStream_t st) {
-  if (!m.stencil || m.W != 256 || getenv_int("IRLMX_COMPACT", 1) == 0) return false;
+// LAY 4: width 256 only)?  From the model's properties when the caller supplied
+// them (irlmx_mdp_properties, checked once per table), else checked on the
+// device per call (bwd_compact_ok_kernel), one int of device memory as the flag;
+// that synchronises the stream.  IRLMX_COMPACT=0 turns the layout off.
+static bool bwd_compact_check(const Model& m, int* flag, hipStream_t st) {
   if (hipMemsetAsync(flag, 0, sizeof(int), st) != hipSuccess) return false;
   hipLaunchKernelGGL(bwd_compact_ok_kernel, dim3((m.S + 255) / 256, m.shared ? 1 : m.B), dim3(256), 0, st,
                      m.row_val, m.W, m.H, m.A, flag);
@@ -2537,6 +2541,11 @@ static bool bwd_compact(const Model& m, int* flag, hipStream_t st) {
   if (hipMemcpyAsync(&h, flag, sizeof(int), hipMemcpyDeviceToHost, st) != hipSuccess) return false;
   if (hipStreamSynchronize(st) != hipSuccess) return false;
   return h == 0;
+}
+static bool bwd_compact(const Model& m, int* flag, hipStream_t st) {
+  if (!m.stencil || m.W != 256 || getenv_int("IRLMX_COMPACT", 1) == 0) return false;
+  if (m.props & IRLMX_PROPS_KNOWN) return (m.props & IRLMX_PROP_COMPACT) != 0;
+  return bwd_compact_check(m, flag, st);
 }
 }  // namespace irlmx
 
@@ -2567,7 +2576,9 @@ extern "C" int irlmx_execution_plan(const irlmx_mdp* mdp, int32_t op, int64_t* p
   ClusterPlan cp;
   const int mode = op == IRLMX_OP_FORWARD ? kModeFwd : kModeBwd;
   bool compact = false;
-  if (op == IRLMX_OP_BACKWARD && m.stencil && m.W == 256) {  // (data-dependent: the table's structure)
+  if (op == IRLMX_OP_BACKWARD && m.stencil && m.W == 256 && (m.props & IRLMX_PROPS_KNOWN)) {
+    compact = bwd_compact(m, nullptr, nullptr);  // (the table's structure, from its properties)
+  } else if (op == IRLMX_OP_BACKWARD && m.stencil && m.W == 256) {  // (data-dependent: checked on the device)
     int* flag = nullptr;
     if (hipMalloc((void**)&flag, sizeof(int)) == hipSuccess) {
       compact = bwd_compact(m, flag, nullptr);
@@ -2730,7 +2741,7 @@ extern "C" int irlmx_backward_maxent(const irlmx_mdp* mdp, const double* reward,
   // calls take the per-sweep shape, whose non-finite bookkeeping is per sweep)
   if (m.stencil && m.A <= kMaxActions && rescale &&
       cluster_plan(m.W, m.H, m.B, kModeBwd, &cp, m.W == 256 && bwd_compact(m, ws.err + 3, st))) {
-    hipLaunchKernelGGL(bwd_growth_kernel, dim3(m.B), dim3(1024), 0, st, ws.wgt, m.S, m.B, ws.growth);
+    hipLaunchKernelGGL(bwd_growth_kernel, dim3(m.B), dim3(1024), 0, st, ws.wgt, m.W, m.S, m.B, ws.growth);
     ClusterArgs ca{};
     ca.W = m.W; ca.H = m.H; ca.S = m.S; ca.A = m.A;
     ca.tab_shared = m.shared ? 1 : 0;
@@ -2795,13 +2806,12 @@ __global__ void np_ell_ascending_kernel(Model m, int* bad) {
   }
 }
 
-// The numpy-order row dots' precondition on an ELL model (above); other
-// layouts visit their entries in column order by construction.  Synchronises.
-static int np_check_ell_rows(const Model& m, const char* fn, hipStream_t st) {
-  if (m.stencil || m.dense) return 0;
+// Whether every ELL row holds its nonzero entries in ascending column order
+// (np_ell_ascending_kernel), into *sorted; synchronises the stream.
+static int ell_rows_sorted(const Model& m, hipStream_t st, bool* sorted) {
   int* flag = nullptr;
   hipError_t e = hipMallocAsync((void**)&flag, sizeof(int), st);
-  if (e != hipSuccess) return hip_fail(e, "numpy-order ELL check");
+  if (e != hipSuccess) return hip_fail(e, "ELL row-order check");
   int h = 0;
   e = hipMemsetAsync(flag, 0, sizeof(int), st);
   if (e == hipSuccess) {
@@ -2811,12 +2821,50 @@ static int np_check_ell_rows(const Model& m, const char* fn, hipStream_t st) {
   }
   (void)hipFreeAsync(flag, st);
   if (e == hipSuccess) e = hipStreamSynchronize(st);
-  if (e != hipSuccess) return hip_fail(e, "numpy-order ELL check");
-  if (h) {
+  if (e != hipSuccess) return hip_fail(e, "ELL row-order check");
+  *sorted = h == 0;
+  return 0;
+}
+
+// The numpy-order row dots' precondition on an ELL model (above); other
+// layouts visit their entries in column order by construction.  From the
+// model's properties when the caller supplied them (irlmx_mdp_properties: once
+// per table), else checked on the device per call (synchronises).
+static int np_check_ell_rows(const Model& m, const char* fn, hipStream_t st) {
+  if (m.stencil || m.dense) return 0;
+  bool sorted = true;
+  if (m.props & IRLMX_PROPS_KNOWN) sorted = (m.props & IRLMX_PROP_ELL_SORTED) != 0;
+  else if (int rc = ell_rows_sorted(m, st, &sorted)) return rc;
+  if (!sorted) {
     set_error("%s: an ELL row holds its nonzero entries out of ascending column order (numpy's order needs "
               "irlmx_dense_to_ell's slot layout)", fn);
     return IRLMX_EINVAL;
   }
+  return 0;
+}
+
+extern "C" int irlmx_mdp_properties(const irlmx_mdp* mdp, int32_t* props, void* stream) {
+  if (int rc = validate(mdp)) return rc;
+  if (!props) { set_error("mdp_properties: props is NULL"); return IRLMX_EINVAL; }
+  Model m = make_model(mdp);
+  m.props = 0;
+  hipStream_t st = (hipStream_t)stream;
+  int32_t p = IRLMX_PROPS_KNOWN;
+  if (m.stencil) {
+    int* flag = nullptr;
+    hipError_t e = hipMallocAsync((void**)&flag, sizeof(int), st);
+    if (e != hipSuccess) return hip_fail(e, "mdp_properties");
+    const bool compact = bwd_compact_check(m, flag, st);
+    e = hipFreeAsync(flag, st);
+    if (e == hipSuccess) e = hipStreamSynchronize(st);
+    if (e != hipSuccess) return hip_fail(e, "mdp_properties");
+    if (compact) p |= IRLMX_PROP_COMPACT;
+  } else if (!m.dense) {
+    bool sorted = false;
+    if (int rc = ell_rows_sorted(m, st, &sorted)) return rc;
+    if (sorted) p |= IRLMX_PROP_ELL_SORTED;
+  }
+  *props = p;
   return 0;
 }
 

@@ -25,6 +25,7 @@ SUCCESS = 0
 OK, NONFINITE, MAXITER = 0, 1, 2
 OP_BACKWARD, OP_FORWARD, OP_SOFT_BACKWARD, OP_VALUE_ITERATION = 1, 2, 3, 4
 PLAN_NO_RESCALE = 0x100
+PROPS_KNOWN, PROP_COMPACT, PROP_ELL_SORTED = 0x40000000, 0x1, 0x2
 EINVAL, EHIP, EWORKSPACE = -1, -2, -3
 COUNTER_NAMES = ("cluster_launches", "grid_launches", "rerun_nonfinite", "rerun_not_resident", "rerun_timeout",
                  "sweep_calls")   # IRLMX_CTR_* order
@@ -47,7 +48,7 @@ class MDPStruct(ctypes.Structure):
         ("k_col", ctypes.c_int32),
         ("batch", ctypes.c_int32),
         ("shared", ctypes.c_int32),
-        ("reserved", ctypes.c_int32),
+        ("props", ctypes.c_int32),
         ("row_val", ctypes.c_void_p),
         ("row_idx", ctypes.c_void_p),
         ("col_idx", ctypes.c_void_p),
@@ -68,6 +69,7 @@ SIGNATURES = {
     "irlmx_last_error": (ctypes.c_char_p, []),
     "irlmx_counters": (ctypes.c_int, [_P, _I32]),
     "irlmx_workspace_bytes": (_SZ, [_MDP, _I32]),
+    "irlmx_mdp_properties": (ctypes.c_int, [_MDP, _P, _P]),
     "irlmx_device_checks_enabled": (ctypes.c_int, []),
     "irlmx_device_check_failures": (_I64, []),
     "irlmx_backward_maxent": (ctypes.c_int, [_MDP, _P, _P, _I32, _P, _P, _P, _SZ, _P]),

@@ -242,6 +242,15 @@ class DeviceMDP:
             s.row_idx = self.row_idx.data_ptr() if self.row_idx is not None else 0
             s.col_idx = self.col_idx.data_ptr() if self.col_idx is not None else 0
             s.col_val = self.col_val.data_ptr() if self.col_val is not None else 0
+            # table properties the calls would otherwise re-check on the device
+            # per call (irlmx_mdp_properties, one synchronising check per model:
+            # the tables of a DeviceMDP are never edited in place): the
+            # compact-weight structure at width 256, ELL row order
+            if self.layout == _lib.LAYOUT_ELL or (self.layout == _lib.LAYOUT_STENCIL5 and self.width == 256):
+                props = ctypes.c_int32(0)
+                _lib.check(_lib.load().irlmx_mdp_properties(ctypes.byref(s), ctypes.byref(props),
+                                                            _lib.stream_ptr(self.device)), "mdp_properties")
+                s.props = props.value
             self._struct = s
         return ctypes.byref(self._struct)
 

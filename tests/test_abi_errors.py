@@ -206,6 +206,19 @@ def test_execution_plan_arguments(lib):
     assert "NO_RESCALE applies to IRLMX_OP_BACKWARD only" in err(lib)
 
 
+def test_mdp_properties_arguments(lib):
+    """irlmx_mdp_properties validates before it touches the device: a NULL model,
+    a NULL result pointer and every bad model are IRLMX_EINVAL."""
+    assert lib.irlmx_mdp_properties(None, fake(), NULL) == EINVAL and err(lib) == "mdp is NULL"
+    m = model()
+    assert lib.irlmx_mdp_properties(ctypes.byref(m), None, NULL) == EINVAL
+    assert err(lib) == "mdp_properties: props is NULL"
+    for case, kw, msg in BAD_MODELS:
+        bad = model(**kw)
+        assert lib.irlmx_mdp_properties(ctypes.byref(bad), fake(), NULL) == EINVAL, case
+        assert msg in err(lib), (case, err(lib))
+
+
 def test_world_builders_and_converters(lib):
     f = fake
     cases = [

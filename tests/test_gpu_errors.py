@@ -141,3 +141,36 @@ def test_numpy_order_rejects_unsorted_ell_rows(dev):
                  lambda: ops.value_iteration(rev, r, 0.9, numpy_order=True)):
         with pytest.raises(Exception, match="ascending column order"):
             call()
+    # the row order is a table property, computed once per model (irlmx_mdp_properties);
+    # with props unknown (0) the entry points check it on the device per call
+    from irlmx import _lib
+    assert good._struct.props == _lib.PROPS_KNOWN | _lib.PROP_ELL_SORTED
+    assert rev._struct.props == _lib.PROPS_KNOWN
+    rev._struct.props = 0
+    with pytest.raises(Exception, match="ascending column order"):
+        ops.backward_maxent_numpy_order(rev, np.exp(r), tm)
+    good._struct.props = 0
+    assert torch.equal(ops.backward_maxent_numpy_order(good, np.exp(r), tm), pi)
+
+
+def test_mdp_properties_compact(dev):
+    """irlmx_mdp_properties on STENCIL5 tables: IcyGridWorld's collapsed backward
+    coefficients have the compact-weight structure, the "stay" variant's (self
+    weights inside the grid) do not; at width 256 the backward plan follows the
+    property, and with props unknown (0) the per-call device check gives the same
+    plan."""
+    import ctypes
+    from irlmx import DeviceMDP, _lib, ops
+    lib = _lib.load()
+    for size in (16, 256):
+        icy = DeviceMDP.icy_gridworld(size, [0.1, 0.3], device=dev)
+        for mdp, compact in ((icy, True), (icy.with_stay(), False)):
+            props = ctypes.c_int32(0)
+            _lib.check(lib.irlmx_mdp_properties(mdp.struct(), ctypes.byref(props), _lib.stream_ptr(dev)), "props")
+            assert props.value == _lib.PROPS_KNOWN | (_lib.PROP_COMPACT if compact else 0), (size, compact)
+            if size == 256:
+                assert mdp._struct.props == props.value
+                plan = ops.execution_plan(mdp, "backward")
+                assert (plan["layout"] == 4) == compact, plan
+                mdp._struct.props = 0
+                assert ops.execution_plan(mdp, "backward") == plan

@@ -653,6 +653,54 @@ def test_solo_backward_rescale_extremes(dev, monkeypatch):
         assert np.max(np.abs(got - ref)) <= 1e-9 * np.max(np.abs(ref)), rv
 
 
+def test_solo_backward_state_feeding_nobody(dev, monkeypatch):
+    """The rescale cadence's decay bound assumes that every state feeds some state
+    with a positive weight (cluster.hip, bwd_growth_kernel).  A 64x64 table in
+    which one interior cell feeds nobody (its four neighbours' moves into it are
+    folded into their "stay" entries, so no row reads it) has no such bound: the
+    kernel then falls back to 16-sweep blocks rescaled every block.  At rewards
+    -5 (decay ~40x per sweep) with +5 on that cell, the solo plan's policy is
+    finite, bit-identical to the per-sweep shape and within 1e-9 of the CSR
+    oracle on the same table."""
+    import scipy.sparse as sp
+    from irlmx import DeviceMDP, ops
+    size = 64
+    n = size * size
+    base = DeviceMDP.icy_gridworld(size, 0.2, device=dev)
+    rv = base.row_val.clone()
+    c = 20 * size + 20
+    for s, k in ((c - 1, 1), (c + 1, 2), (c - size, 3), (c + size, 4)):   # the neighbours' slots that read c
+        rv[0, :, 0, s] += rv[0, :, k, s]
+        rv[0, :, k, s] = 0.0
+    mdp = DeviceMDP(base.layout, n, 4, 1, False, rv, width=size, height=size, device=dev)
+    s_idx = np.arange(n)
+    x, y = s_idx % size, s_idx // size
+    tgt = [s_idx, np.where(x + 1 < size, s_idx + 1, s_idx), np.where(x > 0, s_idx - 1, s_idx),
+           np.where(y + 1 < size, s_idx + size, s_idx), np.where(y > 0, s_idx - size, s_idx)]
+    rvh = rv[0].cpu().numpy()
+    mats = [sp.csr_matrix((np.concatenate([rvh[a, k] for k in range(5)]),
+                           (np.tile(s_idx, 5), np.concatenate(tgt))), shape=(n, n)) for a in range(4)]
+    r = np.full(n, -5.0)
+    r[c] = 5.0
+    tm = ops.terminal_mask([n - 1], n, device=dev)
+    out = {}
+    for name, env in (("solo", {"IRLMX_FUSED_MAX_STATES": "0"}),
+                      ("sweep", {"IRLMX_FUSED_MAX_STATES": "0", "IRLMX_CLUSTER": "0"})):
+        for k in ("IRLMX_FUSED_MAX_STATES", "IRLMX_CLUSTER"):
+            monkeypatch.delenv(k, raising=False)
+        for k, v in env.items():
+            monkeypatch.setenv(k, v)
+        if name == "solo":
+            plan = ops.execution_plan(mdp, "backward")
+            assert plan["C"] == 1 and plan["shape"] == "cluster", plan
+        out[name] = ops.backward_maxent(mdp, r, tm)[0]
+    assert bool(torch.isfinite(out["solo"]).all())
+    assert torch.equal(out["solo"], out["sweep"])
+    ref = O.backward_maxent_csr(mats, [n - 1], r)
+    got = out["solo"].cpu().numpy()
+    assert np.max(np.abs(got - ref)) <= 1e-9 * np.max(np.abs(ref))
+
+
 def test_width256_quads_bit_identical(dev, monkeypatch):
     """Width 256 (config 4's grid): column quads with compact weights (default
     for gridworld tables: three weights per state, cluster.hip LAY 4), the

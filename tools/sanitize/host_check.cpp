@@ -194,6 +194,8 @@ static void error_paths() {
     expect(run_bwd(&b.m, f, f, f, f, f, need), IRLMX_EINVAL, b.msg, b.name);
     int64_t plan[IRLMX_PLAN_LEN];
     expect(irlmx_execution_plan(&b.m, IRLMX_OP_FORWARD, plan), IRLMX_EINVAL, b.msg, b.name);
+    int32_t props = 0;
+    expect(irlmx_mdp_properties(&b.m, &props, nullptr), IRLMX_EINVAL, b.msg, b.name);
     CHECK(irlmx_workspace_bytes(&b.m, IRLMX_OP_FORWARD) == 0, "%s: workspace of an invalid model", b.name);
   }
   expect(run_bwd(&good, nullptr, f, f, f, f, need), IRLMX_EINVAL, "reward is NULL", "null reward");
@@ -215,6 +217,8 @@ static void error_paths() {
   expect(irlmx_execution_plan(&good, IRLMX_OP_FORWARD | IRLMX_PLAN_NO_RESCALE, plan), IRLMX_EINVAL, "NO_RESCALE",
          "no-rescale forward");
   expect(irlmx_execution_plan(&good, IRLMX_OP_FORWARD, nullptr), IRLMX_EINVAL, "plan is NULL", "null plan");
+  expect(irlmx_mdp_properties(nullptr, (int32_t*)f, nullptr), IRLMX_EINVAL, "mdp is NULL", "props null mdp");
+  expect(irlmx_mdp_properties(&good, nullptr, nullptr), IRLMX_EINVAL, "props is NULL", "props null out");
   expect(irlmx_build_icy_gridworld(0, (double*)f, 1, (double*)f, nullptr), IRLMX_EINVAL, "size=0", "icy size");
   expect(irlmx_build_gridworld(50000, 1, (double*)f, nullptr), IRLMX_EINVAL, "size=50000", "grid size");
   expect(irlmx_dense_to_stencil((double*)f, 5, 5, 4, (double*)f, nullptr, nullptr), IRLMX_EINVAL, "off_stencil NULL",
