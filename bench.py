@@ -539,6 +539,8 @@ def main(argv=None):
     svf_p, _, _ = ops.forward_svf(mdp, prime.p_initial, prime.terminal, prime.backward(), max_iter=16)
     prime.update(svf_p)
     prime.last_delta.cpu()
+    if args.full_run:   # the full run's stop test, compaction and working-set updates (BatchedMaxEnt.run)
+        prime.prime_compaction(args.full_run_eps)
     ops.counters()
     del prime, svf_p
     torch.cuda.synchronize()

@@ -379,6 +379,9 @@ def test_backward_numpy_order_64x64_against_restatement(dev, monkeypatch):
     assert np.array_equal(np.argmax(got, axis=1), np.argmax(ref, axis=1))
 
 
+NEAR_TIE = 1e-14   # relative top-two gap below which a soft-VI policy state counts as tied
+
+
 class IcyWorld64:
     """The reference IcyGridWorld(64, 0.2) API the solver drop-ins use: size,
     actions, n_states / n_actions, state_index_transition, p_transition (the
@@ -405,9 +408,13 @@ def test_config2_drop_ins_against_reference(dev):
       discounts 0.7 / 0.9: values bit-identical, sweep counts identical;
       solver.optimal_policy_from_value and solver.optimal_policy
       (solver.py:107-152): np.array_equal with the reference's greedy policy.
-    * maxent.local_causal_action_probabilities (maxent.py:279-341): argmax
-      identical at every state, ties included; policy within 1e-9 (exp / log
-      are the device's); soft-VI sweep count identical."""
+    * maxent.local_causal_action_probabilities (maxent.py:279-341): soft-VI
+      sweep count identical, policy within 1e-9, argmax identical at every
+      state the reference does not tie within a few ulps; at theta = 1, whose
+      ~2,200 mirror-symmetric near-ties (710 exact) are decided by the last bits
+      of exp / log (the device's own, not numpy's AVX-512 ones), the device's
+      action is one of the reference's tied best actions (measured: equal to the
+      reference's at all but 2 of them at discount 0.7)."""
     import maxent as M
     import solver as S
     from irlmx import ops
@@ -426,11 +433,24 @@ def test_config2_drop_ins_against_reference(dev):
             ref = z[c + "__pi"]
             pi = M.local_causal_action_probabilities(P, [n - 1], r, g)
             got, want = np.argmax(pi, axis=1), np.argmax(ref, axis=1)
-            assert np.array_equal(got, want), (c, _argmax_report(got, want))
+            # States whose best two actions the reference separates by at most
+            # NEAR_TIE (relative: a few ulps) are ties decided by the last bits of
+            # ~700 sweeps of exp / log, which the device computes with its own
+            # functions (numpy's AVX-512 exp / log and glibc's log near 1 are not
+            # restated): there the device's action must be one of the reference's
+            # near-tied best actions.  Everywhere else: the reference's argmax.
+            top = np.sort(ref, axis=1)
+            near = (top[:, -1] - top[:, -2]) <= NEAR_TIE * top[:, -1]
+            bad = np.flatnonzero((got != want) & ~near)
+            assert bad.size == 0, (c, _argmax_report(got, want))
+            tied_ok = ref[np.arange(n), got] >= top[:, -1] * (1.0 - NEAR_TIE)
+            assert tied_ok.all(), (c, "argmax outside the near-tied set at", np.flatnonzero(~tied_ok)[:8])
             assert np.max(np.abs(pi - ref)) <= 1e-9 * np.max(np.abs(ref)), c
             _, _, ks, st = ops.soft_backward(mdp, r, O.terminal_reward([n - 1], n), g, numpy_order=True)
             assert int(ks[0]) == int(z[c + "__k_s"]) and int(st[0]) == 0, (c, int(ks[0]))
-            print(f"[c2_64] {c}: argmax equal at {n} states, {int(ks[0])} sweeps, "
+            print(f"[c2_64] {c}: {int(ks[0])} sweeps; argmax equal at all {int((~near).sum())} states not tied "
+                  f"within {NEAR_TIE:g}; at the {int(near.sum())} near-tied states equal at "
+                  f"{int(near.sum()) - int(((got != want) & near).sum())}, the rest one of the tied best actions; "
                   f"max |pi - ref| {np.max(np.abs(pi - ref)):.2e}", flush=True)
             continue
         avg = bool(z[c + "__average"])

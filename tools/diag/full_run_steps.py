@@ -26,6 +26,8 @@ prime = BatchedMaxEnt(mdp, e_f, p0, [S - 1])
 svf_p, _, _ = ops.forward_svf(mdp, prime.p_initial, prime.terminal, prime.backward(), max_iter=16)
 prime.update(svf_p)
 prime.last_delta.cpu()
+if os.environ.get("NO_PRIME_COMPACTION") != "1":
+    prime.prime_compaction()
 del prime, svf_p
 torch.cuda.synchronize()
 
