@@ -37,6 +37,11 @@ constexpr size_t kMaxLdsBytes = 160 * 1024;  // LDS per CU (one workgroup per CU
 // cluster.hip, p_max.)
 constexpr int kSumSlots = kRescaleEvery < 8 ? 8 : kRescaleEvery + 1;
 static_assert(kSumSlots > kRescaleEvery, "summary slots must outlast the rescale period");
+// Rows of an instance's summary granules (sgran): [0, kSumSlots) block summaries,
+// kSumSlots the tiles' XCC ids, kSumSlots + 1 the forward's full convergence
+// flags of a replayed block (cluster.hip, "cheap convergence proof").
+constexpr int kSumRows = kSumSlots + 2;
+constexpr int kXccRow = kSumSlots, kFullRow = kSumSlots + 1;
 constexpr size_t kClusterStaticLds = 128;     // cluster_kernel's own __shared__ variables (resident flag, stamps)
 constexpr int kModeFwd = 0;
 constexpr int kModeBwd = 1;
@@ -60,7 +65,7 @@ struct ClusterArgs {
   long long n_sweeps;      // backward: collapsed sweeps (2S - 1)
   int rescale;
   unsigned long long* gran;   // [B][gran_inst_len] x 16-byte tagged granule pairs (halo rows, see kGranRowPad)
-  unsigned long long* sgran;  // [B][kSumSlots + 1][H] x 16-byte tagged granule pairs (tile summaries, XCC ids)
+  unsigned long long* sgran;  // [B][kSumRows][H] x 16-byte tagged granule pairs (tile summaries, XCC ids, full flags)
   int xcd_group;           // number the tiles of an instance within one XCD group
   unsigned salt;           // per-launch granule tag salt
   int* err;                // [0]: exchange timeout (1), non-finite (2), not co-resident (4); [1..2]: rendezvous
@@ -105,10 +110,10 @@ constexpr int kGatherPerThread = 4;
 #define IRLMX_GRAN_ROW_PAD 0
 #endif
 #ifndef IRLMX_GRAN_PAR_PAD
-#define IRLMX_GRAN_PAR_PAD 24
+#define IRLMX_GRAN_PAR_PAD 0
 #endif
 #ifndef IRLMX_GRAN_INST_PAD
-#define IRLMX_GRAN_INST_PAD 40
+#define IRLMX_GRAN_INST_PAD 0
 #endif
 constexpr int kGranRowPad = IRLMX_GRAN_ROW_PAD;                   // extra granules per row (8: one 128-B line)
 __host__ __device__ inline size_t gran_par_len(int W, int H) {

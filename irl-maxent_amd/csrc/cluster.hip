@@ -45,6 +45,7 @@
 #include <cmath>
 #include <cstdio>
 #include <cstdlib>
+#include <type_traits>
 
 #include "cluster.h"
 #include "common.h"
@@ -128,6 +129,15 @@ __global__ void __launch_bounds__(NT) cluster_kernel(ClusterArgs a) {
   constexpr int HW = COLS ? WT / CPL : 1;                // COLS: lanes per band
   constexpr int NB = COLS ? NT / HW : 1;                 // COLS: bands
   constexpr int QW = CPL / 2;                            // COLS: double2 per lane per row
+#ifndef IRLMX_FWD_PROOF
+#define IRLMX_FWD_PROOF 1
+#endif
+  // Forward, column layouts: per-sweep bookkeeping on band row kProofRow only
+  // (the cheap proof of "not converged"; the block loop replays a block with
+  // full bookkeeping when some sweep is left unproven).  IRLMX_FWD_PROOF=0: full
+  // bookkeeping every sweep, as before round 6.
+  constexpr bool kProof = MODE == kModeFwd && COLS && IRLMX_FWD_PROOF;
+  constexpr int kProofRow = RW / 2;
 #ifndef IRLMX_LDS_SIDES
 #define IRLMX_LDS_SIDES -1
 #endif
@@ -272,6 +282,17 @@ __global__ void __launch_bounds__(NT) cluster_kernel(ClusterArgs a) {
   }
   // one sweep's new value from the weighted sum: forward p0 + sum, backward the sum
   auto finish = [&](int j, double acc) { return MODE == kModeFwd ? c0[MODE == kModeFwd ? j : 0] + acc : acc; };
+  // forward: does any slot of this wave hold a nonzero p0 (NaN counts)?  Wave-uniform (SGPR).
+  bool wave_p0 = true;
+  if constexpr (MODE == kModeFwd) {
+    bool mine = false;
+#pragma unroll
+    for (int j = 0; j < SPT; ++j) mine |= !(c0[MODE == kModeFwd ? j : 0] == 0.0);
+#ifndef IRLMX_FWD_P0_SKIP
+#define IRLMX_FWD_P0_SKIP 1
+#endif
+    wave_p0 = !IRLMX_FWD_P0_SKIP || __builtin_amdgcn_readfirstlane(__builtin_amdgcn_ballot_w64(mine) != 0ull ? 1 : 0) != 0;
+  }
   for (int i = tid; i < (COLS ? 1 : 2) * blen; i += NT) bufA[i] = 0.0;
   for (int i = tid; i < kBndLen; i += NT) bnd[i] = make_double2(0.0, 0.0);
   if constexpr (CW) {
@@ -455,8 +476,18 @@ __global__ void __launch_bounds__(NT) cluster_kernel(ClusterArgs a) {
   auto edge_row = [&](int par, int band, int e) {
     return reinterpret_cast<double*>(bnd + (((size_t)par * (NB + 2) + band) * 2 + e) * HW * QW);
   };
+  // p0tag (std::integral_constant<bool, P0>): with P0 false the forward's "p0 +"
+  // is left out -- exact where every p0 of the wave's slots is +-0: the FMA
+  // chain starts from fma(w, v, +0.0), which is never -0.0, so 0.0 + acc == acc
+  // bit for bit (NaN and inf included).
+  //
+  // fulltag (std::integral_constant<bool, FULL>): the forward's owned-delta
+  // bookkeeping on every owned slot (FULL) or only on the slots of band row
+  // kProofRow, the cheap proof of "not converged" (see the block loop).
   auto cols_sweep = [&](const double (&src)[COLS ? SPT : 1], double (&dst)[COLS ? SPT : 1], int i,
-                        unsigned& flags) {
+                        unsigned& flags, auto p0tag, auto fulltag) {
+    constexpr bool kP0 = decltype(p0tag)::value;
+    constexpr bool kFull = decltype(fulltag)::value;
     if constexpr (COLS) {
       const unsigned ob = slot_bits(own_bits);
       double dmax = 0.0;
@@ -485,8 +516,30 @@ __global__ void __launch_bounds__(NT) cluster_kernel(ClusterArgs a) {
       // sweep counts.  Round 5: at 12 states per lane too (config 3's and the
       // batched causal forward; two VGPRs spill, outside the sweep loop): B = 64
       // at 128x128, 3,000 sweeps 3.19 -> 3.01 ms, three alternations on one box.
+#ifndef IRLMX_FWD_BALLOT_ACCOUNT
+#define IRLMX_FWD_BALLOT_ACCOUNT 0
+#endif
+#ifndef IRLMX_FWD_NO_ACCOUNT
+#define IRLMX_FWD_NO_ACCOUNT 0   // timing experiments only: every sweep counts as not converged
+#endif
+      // IRLMX_FWD_BALLOT_ACCOUNT=1 (round 6, measured slower): no branch and no
+      // select -- per slot one f64 subtract and one compare whose lane mask (a
+      // ballot, SGPRs) is ANDed with the slot's ownership and ORed into a
+      // wave-uniform mask, the sweep one straight-line block.  The same bit as
+      // the fmax form's (NaN > eps is false, as fmax drops NaN), but each
+      // compare-to-SGPR feeds a scalar OR: config 3's plan 11.4k -> 14.4k cycles
+      // of sweeps per 8-sweep block, one 128x128 instance 6.9k -> 9.1k.
+      constexpr bool kBallotAccount = MODE == kModeFwd && IRLMX_FWD_BALLOT_ACCOUNT;
+      unsigned long long anyv = 0ull;
       auto account = [&](int j, double nv, double self) {
-        if constexpr (MODE == kModeFwd && kUniformSlots && SPT <= IRLMX_FWD_BRANCH_SPT_MAX && IRLMX_FWD_BRANCH_ACCOUNT) {
+        if (!kFull && j / CPL != kProofRow) return;   // (compile-time after unrolling)
+        if constexpr (MODE == kModeFwd && IRLMX_FWD_NO_ACCOUNT) {
+          (void)j; (void)nv; (void)self;
+        } else if constexpr (kBallotAccount) {
+          bool big = ((ob >> j) & 1u) != 0u;
+          big = big & (fabs(nv - self) > eps);
+          anyv |= __builtin_amdgcn_ballot_w64(big);
+        } else if constexpr (MODE == kModeFwd && kUniformSlots && SPT <= IRLMX_FWD_BRANCH_SPT_MAX && IRLMX_FWD_BRANCH_ACCOUNT) {
           if ((ob >> j) & 1u) {
             asm volatile("");
             dmax = fmax(dmax, fabs(nv - self));
@@ -640,7 +693,7 @@ __global__ void __launch_bounds__(NT) cluster_kernel(ClusterArgs a) {
           }
 #pragma unroll
           for (int c = 0; c < CPL; ++c) {
-            dst[jr * CPL + c] = finish(jr * CPL + c, acc[c]);
+            dst[jr * CPL + c] = kP0 ? finish(jr * CPL + c, acc[c]) : acc[c];
             account(jr * CPL + c, dst[jr * CPL + c], v[c]);
           }
         }
@@ -691,13 +744,15 @@ __global__ void __launch_bounds__(NT) cluster_kernel(ClusterArgs a) {
         if constexpr (kLazy) edges_in(1, false);
         rows(0, 0);
       }
-      if (MODE == kModeFwd) flags |= ((dmax > eps) ? 1u : 0u) << i;
+      if constexpr (MODE == kModeFwd && IRLMX_FWD_NO_ACCOUNT) flags |= 1u << i;
+      else if constexpr (kBallotAccount) flags |= (anyv != 0ull ? 1u : 0u) << i;
+      else if (MODE == kModeFwd) flags |= ((dmax > eps) ? 1u : 0u) << i;
     }
   };
 
   // Halo exchange in tagged granules (cluster.h): this instance's region of
-  // a.gran is [2 parities][H rows][W + kGranRowPad] x 16 B (cluster.h), of a.sgran [kSumSlots + 1][H tiles] x 16 B
-  // (summaries by block % kSumSlots, then the XCC ids).
+  // a.gran is [2 parities][H rows][W + kGranRowPad] x 16 B (cluster.h), of a.sgran [kSumRows][H tiles] x 16 B
+  // (summaries by block % kSumSlots, then the XCC ids and the full forward flags).
   const size_t gpl = gran_par_len(W, H);
   const Gran rg = gran_rsrc(a.gran + (size_t)inst * 2 * gran_inst_len(W, H), 32u * (unsigned)gpl);
   constexpr int kRG = WT ? WT + kGranRowPad : 0;  // granules per row (compile-time where the width is)
@@ -705,7 +760,7 @@ __global__ void __launch_bounds__(NT) cluster_kernel(ClusterArgs a) {
   const unsigned gbase = (unsigned)e0 * rgw;
   // granule index of extended-tile state l in the parity-0 half
   auto gidx = [&](int l) { return gbase + (unsigned)(l / W) * rgw + (unsigned)(l % W); };
-  const Gran rs = gran_rsrc(a.sgran + (size_t)inst * 2 * (kSumSlots + 1) * a.H, 16u * (kSumSlots + 1) * (unsigned)a.H);
+  const Gran rs = gran_rsrc(a.sgran + (size_t)inst * 2 * kSumRows * a.H, 16u * kSumRows * (unsigned)a.H);
   const int ng0 = own0, ng = own0 + (E - own1);  // ghost states: [0, own0) and [own1, E)
   const unsigned salt = (a.salt & 0xFFFu) << 20;  // per call: a stale granule of an earlier call never matches
   // Hand-off store form: write-through (sc1) in general; plain stores (kept in
@@ -717,13 +772,13 @@ __global__ void __launch_bounds__(NT) cluster_kernel(ClusterArgs a) {
     asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
     xcc &= 0xFu;
     const unsigned htag = salt | 0xFFFFFu;
-    if (tid == 0) gran_store(rs, ((unsigned)kSumSlots * (unsigned)a.H + (unsigned)tile) * 16u, xcc, htag, false);
+    if (tid == 0) gran_store(rs, ((unsigned)kXccRow * (unsigned)a.H + (unsigned)tile) * 16u, xcc, htag, false);
     bool ok = true;
     if (tid < kWave) {
       unsigned long long diff = 0ull;
       for (int t0 = 0; t0 < a.C; t0 += kWave) {
         unsigned long long v[1] = {xcc};
-        unsigned off[1] = {((unsigned)kSumSlots * (unsigned)a.H + (unsigned)(t0 + tid)) * 16u};
+        unsigned off[1] = {((unsigned)kXccRow * (unsigned)a.H + (unsigned)(t0 + tid)) * 16u};
         ok &= gran_gather<1>(rs, rs, off, t0 + tid < a.C ? 1u : 0u, htag, v, a.gather_ticks);
         diff |= v[0] ^ xcc;
       }
@@ -767,11 +822,11 @@ __global__ void __launch_bounds__(NT) cluster_kernel(ClusterArgs a) {
     if constexpr (COLS) {
       int i = 0;
       for (; i + 1 < n; i += 2) {
-        cols_sweep(cv, cw, i, fl);
-        cols_sweep(cw, cv, i + 1, fl);
+        cols_sweep(cv, cw, i, fl, std::true_type{}, std::true_type{});
+        cols_sweep(cw, cv, i + 1, fl, std::true_type{}, std::true_type{});
       }
       if (i < n) {
-        cols_sweep(cv, cw, i, fl);
+        cols_sweep(cv, cw, i, fl, std::true_type{}, std::true_type{});
 #pragma unroll
         for (int j = 0; j < (COLS ? SPT : 1); ++j) cv[j] = cw[j];
       }
@@ -788,8 +843,29 @@ __global__ void __launch_bounds__(NT) cluster_kernel(ClusterArgs a) {
     __syncthreads();
     reload(cur);
   };
+  // COLS: the T_m sweeps of block m in registers (fulltag: see cols_sweep)
+  int Tm = T;
+  auto block_sweeps = [&](unsigned& fl, auto fulltag) {
+    if constexpr (COLS) {
+      auto go = [&](auto p0tag) {
+        int i = 0;
+        for (; i + 1 < Tm; i += 2) {
+          cols_sweep(cv, cw, i, fl, p0tag, fulltag);
+          cols_sweep(cw, cv, i + 1, fl, p0tag, fulltag);
+        }
+        if (i < Tm) {
+          cols_sweep(cv, cw, i, fl, p0tag, fulltag);
+#pragma unroll
+          for (int j = 0; j < (COLS ? SPT : 1); ++j) cv[j] = cw[j];
+        }
+      };
+      // (the full-bookkeeping replay, rare, keeps the p0 add everywhere: one copy less of the loop)
+      if (MODE == kModeFwd && (decltype(fulltag)::value && kProof || wave_p0)) go(std::true_type{});
+      else go(std::false_type{});
+    }
+  };
   for (int m = 0;; ++m) {
-    int Tm = T;
+    Tm = T;
     if (MODE == kModeBwd) Tm = (int)min<long long>((long long)T, total - done);
     // ---- T_m sweeps on chip ----------------------------------------------
     unsigned flags = 0;
@@ -801,16 +877,10 @@ __global__ void __launch_bounds__(NT) cluster_kernel(ClusterArgs a) {
     const bool resc = MODE == kModeBwd && a.rescale && (rescale_in <= 1 || done + Tm >= total);
     double mxd = 0.0;
     if constexpr (COLS) {
-      int i = 0;
-      for (; i + 1 < Tm; i += 2) {
-        cols_sweep(cv, cw, i, flags);
-        cols_sweep(cw, cv, i + 1, flags);
-      }
-      if (i < Tm) {
-        cols_sweep(cv, cw, i, flags);
-#pragma unroll
-        for (int j = 0; j < (COLS ? SPT : 1); ++j) cv[j] = cw[j];
-      }
+      // forward: the p0 add only in waves holding a nonzero p0 (the start states:
+      // one wave of the launch at config 3), a wave-uniform scalar branch around
+      // the whole block, so each sweep stays one straight-line block
+      block_sweeps(flags, std::integral_constant<bool, !kProof>{});
 #ifndef IRLMX_POST_SWEEP_BARRIER
 #define IRLMX_POST_SWEEP_BARRIER 0
 #endif
@@ -968,7 +1038,7 @@ __global__ void __launch_bounds__(NT) cluster_kernel(ClusterArgs a) {
     if (tid == 0) red32[m & 1] = 0u;  // next-but-one block's tile summary (read above)
     stamp(2);
     if (MODE == kModeFwd) {
-      const unsigned msk = summary;
+      unsigned msk = summary;
       if (msk >> 31) {
         // a non-finite value: every tile of the instance sees the same bit and
         // leaves; the host reruns the call with exact NaN bookkeeping
@@ -978,6 +1048,51 @@ __global__ void __launch_bounds__(NT) cluster_kernel(ClusterArgs a) {
       }
       int conv = 0;
       const unsigned live = (1u << Tm) - 1;
+      if constexpr (kProof) {
+        // Cheap convergence proof.  The block's sweeps kept the owned-delta
+        // bookkeeping on band row kProofRow only: a set bit i proves "some owned
+        // |delta| > eps at sweep i" (a subset's maximum is at most the
+        // maximum), a clear one proves nothing.  If every sweep is proven, the
+        // instance is not converged anywhere in the block -- the common case.
+        // Otherwise (every tile sees the same OR), every tile replays the block
+        // from its start with full bookkeeping -- registers from the LDS
+        // snapshot; the tile buffer keeps the ghost rows just gathered -- which
+        // recomputes the same values bit for bit, and the tiles exchange the
+        // exact flags in a second summary round (row kFullRow).  The stop
+        // decision below then uses those.  Typically two blocks of a call
+        // replay: the first (the start distribution has not reached the proof
+        // rows yet) and the stopping one.
+        if ((msk & live) != live) {
+          if (tid == 0) { lflag[2] = 0; lflag[3] = 0; }
+          const unsigned xb = slot_bits(ext_bits);
+#pragma unroll
+          for (int j = 0; j < (COLS ? SPT : 1); ++j) cv[j] = ((xb >> j) & 1u) ? snap[slot_state(j)] : 0.0;
+          unsigned ff = 0;
+          block_sweeps(ff, std::true_type{});
+          const unsigned wf = wave_reduce_u32<1>(ff) & live;
+          __syncthreads();   // (lflag[2..3] zeroed; every wave's sweeps done)
+          if ((tid & (kWave - 1)) == 0 && wf) atomicOr(reinterpret_cast<unsigned*>(&lflag[2]), wf);
+          __syncthreads();
+          bool ok2 = true;
+          if (!solo) {
+            if (tid == 0)
+              gran_store(rs, ((unsigned)kFullRow * (unsigned)a.H + (unsigned)tile) * 16u, (unsigned)lflag[2], tag,
+                         plain);
+            if (tid < a.C) {
+              unsigned long long v[1];
+              const unsigned off[1] = {((unsigned)kFullRow * (unsigned)a.H + (unsigned)tid) * 16u};
+              ok2 = gran_gather<1>(rs, rs, off, 1u, tag, v, a.gather_ticks);
+              if (ok2) atomicOr(reinterpret_cast<unsigned*>(&lflag[3]), (unsigned)v[0]);
+            }
+          } else if (tid == 0) {
+            lflag[3] = lflag[2];
+          }
+          if (!ok2) { lflag[0] = 1; atomicOr(a.err, 1); }
+          __syncthreads();
+          if (lflag[0]) return;  // exchange timed out (reported through a.err)
+          msk = (unsigned)__builtin_amdgcn_readfirstlane(lflag[3]);
+        }
+      }
       if ((msk & live) != live || (a.max_iter > 0 && done + Tm >= a.max_iter)) {
         for (int i = 0; i < Tm; ++i) {
           const bool cap = a.max_iter > 0 && done + i + 1 >= a.max_iter;

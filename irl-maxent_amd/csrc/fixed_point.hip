@@ -131,8 +131,8 @@ struct Ws {
   // cluster shape (stencil layouts too large for one CU); sizes as carve() takes them:
   unsigned long long* gran;   // cluster: [B][gran_inst_len(W, H)] x 16 B (two padded halo parities, cluster.h);
                               // grid: [B][3][S] x 16 B; dense grid: [B][2][S] x 16 B
-  unsigned long long* sgran;  // cluster: [B][kSumSlots + 1][H] x 16 B (tile summaries by block % kSumSlots,
-                              // then the XCC ids); grid: [B][4][bpi]; dense grid: [B][bpi] x 16 B
+  unsigned long long* sgran;  // cluster: [B][kSumRows][H] x 16 B (tile summaries by block % kSumSlots,
+                              // then the XCC ids and the forward's full flags, cluster.h); grid: [B][4][bpi]; dense grid: [B][bpi] x 16 B
   unsigned long long* growth; // [2][B] growth / decay bounds (bwd_growth_kernel)
   int* err;                   // [4]: error bits, rendezvous counters
   size_t total;
@@ -180,12 +180,12 @@ static Ws carve(const Model& m, int op, void* base) {
   const bool gr = sweep && grid_plan(m, op, &gp);
   DenseGridPlan dp{0, 0, 0, 0};
   const bool dg = sweep && dense_grid(m, op, &dp);
-  // cluster halo exchange: [B][gran_inst_len] and [B][kSumSlots + 1][H] 16-byte granule pairs;
+  // cluster halo exchange: [B][gran_inst_len] and [B][kSumRows][H] 16-byte granule pairs;
   // grid shape: [B][3][S] value and [B][3][bpi] block-delta granules;
   // dense grid shape: [B][2][S] value and [B][bpi] XCC-id granules
   const size_t gcl = cl ? B * gran_inst_len(m.W, m.H) * 16 : 0;   // cluster.h kGranRowPad layout
   w.gran = (unsigned long long*)take(std::max(gcl, dg ? 2 * B * S * 16 : (gr ? 3 * B * S * 16 : 0)));
-  w.sgran = (unsigned long long*)take(cl ? (kSumSlots + 1) * B * (size_t)m.H * 16
+  w.sgran = (unsigned long long*)take(cl ? kSumRows * B * (size_t)m.H * 16
                                          : (gr ? 4 * B * (size_t)gp.bpi * 16 : (dg ? B * (size_t)dp.bpi * 16 : 0)));
   w.growth = (unsigned long long*)take(cl ? 2 * B * sizeof(unsigned long long) : 0);
   w.err = (int*)take(cl || gr || dg ? 4 * sizeof(int) : 0);

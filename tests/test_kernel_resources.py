@@ -3,12 +3,14 @@ config-4 backward spilled 27 VGPRs, the config-3 forward 2).  hipcc's
 kernel-resource-usage remarks for every instantiation of csrc/cluster.hip
 (tools/kernel_resources.py); CPU only (hipcc cross-compiles gfx950).
 
-Three instantiations may spill a few VGPRs: config 4's backward,
+A few instantiations may spill a few VGPRs: config 4's backward,
 cluster_kernel<1, 20, 256, 4, 512> (compact weights, 20 states per lane: 255
 VGPRs and no spill since round 5's schedule change, at the limit),
 config 3's forward, cluster_kernel<0, 12, 128, 2, 512> (owned-delta bookkeeping
-as scalar branches), and the same forward in column quads at width 256 (only
-planned when forced), all at 256 VGPRs.  Their spills must stay out of the
+as scalar branches; since round 6 three copies of the block's sweeps: the
+proof-row bookkeeping with and without the p0 add, and the full-bookkeeping
+replay), the same forward at width 64 and in column quads at widths 128 and
+256 (only planned when forced), all at 256 VGPRs.  Their spills must stay out of the
 sweeps: no basic block that holds the stencil's fp64 FMAs has a scratch access,
 and the loop's FMAs are all there (at least one sweep's: states x 5)."""
 
@@ -24,8 +26,9 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 SRC = os.path.join(ROOT, "irl-maxent_amd", "csrc", "cluster.hip")
 HIPCC = shutil.which("hipcc") or "/opt/rocm/bin/hipcc"
 # instantiation -> max spilled VGPRs, allowed outside the sweep loop only
-ALLOWED = {"cluster_kernel<1, 20, 256, 4, 512>": 4, "cluster_kernel<0, 12, 128, 2, 512>": 4,
-           "cluster_kernel<0, 12, 256, 3, 512>": 4}
+ALLOWED = {"cluster_kernel<1, 20, 256, 4, 512>": 4, "cluster_kernel<0, 12, 128, 2, 512>": 8,
+           "cluster_kernel<0, 12, 64, 2, 512>": 4, "cluster_kernel<0, 12, 256, 3, 512>": 8,
+           "cluster_kernel<0, 12, 128, 3, 512>": 8}
 MANGLED = {k: "_ZN5irlmx14cluster_kernelILi{}ELi{}ELi{}ELi{}ELi512EEEvNS_11ClusterArgsE".format(
                *re.findall(r"\d+", k)[:4]) for k in ALLOWED}
 
