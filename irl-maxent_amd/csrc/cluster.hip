@@ -1367,8 +1367,16 @@ bool cluster_plan(int W, int H, int B, int mode, ClusterPlan* out, bool compact)
   const int rows_cap = nt * spt_max / W;
   double best = 1e300;
   bool ok = false;
+  // Column-pair backward at width 128: plans with G = 8 ghost rows measured as
+  // fast as or faster than the cost model's choice at every working-set size of
+  // the full run (tools/diag/g8_plans.py, one MI355X: 9-16 instances 17.5 ->
+  // 16.4 ms, 17-24 20.4 -> 19.2, 33-40 24.3 -> 23.2; within 0.7 % elsewhere),
+  // so the search is restricted to G = 8 there, unless nothing fits.
+  const bool prefer8 = !fG && mode == kModeBwd && layout == 2 && W == 128 && env_int("IRLMX_PLAN_G8", 1) != 0;
+  for (int pass = prefer8 ? 0 : 1; pass < 2 && !ok; ++pass)
   for (int G = kTMax; G >= 1; --G) {
     if (fG && G != fG) continue;
+    if (pass == 0 && G != 8) continue;
     for (int R = std::min(H, rows_cap - 2 * G); R >= 1; --R) {
       if (fR && R != fR) continue;
       const int C = (H + R - 1) / R;
