@@ -843,17 +843,20 @@ __global__ void __launch_bounds__(NT) cluster_kernel(ClusterArgs a) {
     __syncthreads();
     reload(cur);
   };
-  // COLS: the T_m sweeps of block m in registers (fulltag: see cols_sweep)
-  int Tm = T;
-  auto block_sweeps = [&](unsigned& fl, auto fulltag) {
-    if constexpr (COLS) {
+  // COLS forward: the n sweeps of a block in registers (fulltag: see cols_sweep).
+  // (The backward keeps its own copy of this loop in the block loop: written
+  // through this lambda, its schedule changed -- fewer interior FMAs between the
+  // band-edge stores and the barrier -- and config 3's backward lost 7.8 %,
+  // 22.0 -> 23.8 ms, profiles/r06_forward_ab.txt.)
+  auto block_sweeps = [&](unsigned& fl, const int n, auto fulltag) {
+    if constexpr (COLS && MODE == kModeFwd) {
       auto go = [&](auto p0tag) {
         int i = 0;
-        for (; i + 1 < Tm; i += 2) {
+        for (; i + 1 < n; i += 2) {
           cols_sweep(cv, cw, i, fl, p0tag, fulltag);
           cols_sweep(cw, cv, i + 1, fl, p0tag, fulltag);
         }
-        if (i < Tm) {
+        if (i < n) {
           cols_sweep(cv, cw, i, fl, p0tag, fulltag);
 #pragma unroll
           for (int j = 0; j < (COLS ? SPT : 1); ++j) cv[j] = cw[j];
@@ -865,7 +868,7 @@ __global__ void __launch_bounds__(NT) cluster_kernel(ClusterArgs a) {
     }
   };
   for (int m = 0;; ++m) {
-    Tm = T;
+    int Tm = T;
     if (MODE == kModeBwd) Tm = (int)min<long long>((long long)T, total - done);
     // ---- T_m sweeps on chip ----------------------------------------------
     unsigned flags = 0;
@@ -877,10 +880,23 @@ __global__ void __launch_bounds__(NT) cluster_kernel(ClusterArgs a) {
     const bool resc = MODE == kModeBwd && a.rescale && (rescale_in <= 1 || done + Tm >= total);
     double mxd = 0.0;
     if constexpr (COLS) {
-      // forward: the p0 add only in waves holding a nonzero p0 (the start states:
-      // one wave of the launch at config 3), a wave-uniform scalar branch around
-      // the whole block, so each sweep stays one straight-line block
-      block_sweeps(flags, std::integral_constant<bool, !kProof>{});
+      if constexpr (MODE == kModeBwd) {
+        int i = 0;
+        for (; i + 1 < Tm; i += 2) {
+          cols_sweep(cv, cw, i, flags, std::false_type{}, std::true_type{});
+          cols_sweep(cw, cv, i + 1, flags, std::false_type{}, std::true_type{});
+        }
+        if (i < Tm) {
+          cols_sweep(cv, cw, i, flags, std::false_type{}, std::true_type{});
+#pragma unroll
+          for (int j = 0; j < (COLS ? SPT : 1); ++j) cv[j] = cw[j];
+        }
+      } else {
+        // forward: the p0 add only in waves holding a nonzero p0 (the start states:
+        // one wave of the launch at config 3), a wave-uniform scalar branch around
+        // the whole block, so each sweep stays one straight-line block
+        block_sweeps(flags, Tm, std::integral_constant<bool, !kProof>{});
+      }
 #ifndef IRLMX_POST_SWEEP_BARRIER
 #define IRLMX_POST_SWEEP_BARRIER 0
 #endif
@@ -1068,7 +1084,7 @@ __global__ void __launch_bounds__(NT) cluster_kernel(ClusterArgs a) {
 #pragma unroll
           for (int j = 0; j < (COLS ? SPT : 1); ++j) cv[j] = ((xb >> j) & 1u) ? snap[slot_state(j)] : 0.0;
           unsigned ff = 0;
-          block_sweeps(ff, std::true_type{});
+          block_sweeps(ff, Tm, std::true_type{});
           const unsigned wf = wave_reduce_u32<1>(ff) & live;
           __syncthreads();   // (lflag[2..3] zeroed; every wave's sweeps done)
           if ((tid & (kWave - 1)) == 0 && wf) atomicOr(reinterpret_cast<unsigned*>(&lflag[2]), wf);

@@ -246,9 +246,11 @@ class DeviceMDP:
             # per call (irlmx_mdp_properties, one synchronising check per model:
             # the tables of a DeviceMDP are never edited in place): the
             # compact-weight structure at width 256, ELL row order
-            if self.layout == _lib.LAYOUT_ELL or (self.layout == _lib.LAYOUT_STENCIL5 and self.width == 256):
+            lib = _lib.load()
+            if hasattr(lib, "irlmx_mdp_properties") and (   # (an older IRLMX_LIB variant build may lack it)
+                    self.layout == _lib.LAYOUT_ELL or (self.layout == _lib.LAYOUT_STENCIL5 and self.width == 256)):
                 props = ctypes.c_int32(0)
-                _lib.check(_lib.load().irlmx_mdp_properties(ctypes.byref(s), ctypes.byref(props),
+                _lib.check(lib.irlmx_mdp_properties(ctypes.byref(s), ctypes.byref(props),
                                                             _lib.stream_ptr(self.device)), "mdp_properties")
                 s.props = props.value
             self._struct = s
