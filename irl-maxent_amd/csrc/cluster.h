@@ -101,25 +101,31 @@ typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
 constexpr int kGatherPerThread = 4;
 
 // Halo granule layout per instance: [2 parities][S states (+ kGranRowPad per
-// row)] x 16 B, the parities and instances a few 128-B lines further apart than
-// their power-of-two sizes (24 and 40 granules).  Measured on one MI355X
-// (tools/diag/gran_layout_ab.sh): the config-4 backward's hand-off wait 3.1k ->
-// 2.5k cycles per block, 200 -> 192 ms per launch; config 3 unchanged (22.4-22.5
-// ms).  Padding every row as well (8 or 16 granules) gave the same times.
+// row)] x 16 B.  At width 128 the parities and the instances sit a few 128-B
+// lines further apart than their power-of-two sizes (24 and 40 granules); other
+// widths keep the power-of-two distances.  Measured (DESIGN.md section 4 "Halo
+// granule layout", profiles/r06_pad_ab.txt, r06_pmc_writeback.txt): the offsets
+// make the L2 write dirty granule lines back 4x as often (config 3's backward
+// 3.1 -> 12 GB of WRITE_SIZE per launch, no extra evictions) yet run config 3's
+// backward 0.5-0.7 % faster on three boxes; at width 256 (config 4) the
+// unpadded layout is ~1 % faster.  IRLMX_GRAN_PAR_PAD / _INST_PAD (>= 0) force
+// one layout at every width.
 #ifndef IRLMX_GRAN_ROW_PAD
 #define IRLMX_GRAN_ROW_PAD 0
 #endif
 #ifndef IRLMX_GRAN_PAR_PAD
-#define IRLMX_GRAN_PAR_PAD 0
+#define IRLMX_GRAN_PAR_PAD -1
 #endif
 #ifndef IRLMX_GRAN_INST_PAD
-#define IRLMX_GRAN_INST_PAD 0
+#define IRLMX_GRAN_INST_PAD -1
 #endif
 constexpr int kGranRowPad = IRLMX_GRAN_ROW_PAD;                   // extra granules per row (8: one 128-B line)
+__host__ __device__ inline size_t gran_par_pad(int W) { return IRLMX_GRAN_PAR_PAD >= 0 ? IRLMX_GRAN_PAR_PAD : (W == 128 ? 24 : 0); }
+__host__ __device__ inline size_t gran_inst_pad(int W) { return IRLMX_GRAN_INST_PAD >= 0 ? IRLMX_GRAN_INST_PAD : (W == 128 ? 40 : 0); }
 __host__ __device__ inline size_t gran_par_len(int W, int H) {
-  return (size_t)H * (W + kGranRowPad) + IRLMX_GRAN_PAR_PAD;
+  return (size_t)H * (W + kGranRowPad) + gran_par_pad(W);
 }
-__host__ __device__ inline size_t gran_inst_len(int W, int H) { return 2 * gran_par_len(W, H) + IRLMX_GRAN_INST_PAD; }
+__host__ __device__ inline size_t gran_inst_len(int W, int H) { return 2 * gran_par_len(W, H) + gran_inst_pad(W); }
 
 // A granule buffer: its descriptor (and, in IRLMX_DEVICE_CHECKS builds, its
 // byte length for the offset checks).

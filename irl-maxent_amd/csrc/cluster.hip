@@ -1388,7 +1388,9 @@ bool cluster_plan(int W, int H, int B, int mode, ClusterPlan* out, bool compact)
   // the full run (tools/diag/g8_plans.py, one MI355X: 9-16 instances 17.5 ->
   // 16.4 ms, 17-24 20.4 -> 19.2, 33-40 24.3 -> 23.2; within 0.7 % elsewhere),
   // so the search is restricted to G = 8 there, unless nothing fits.
-  const bool prefer8 = !fG && mode == kModeBwd && layout == 2 && W == 128 && env_int("IRLMX_PLAN_G8", 1) != 0;
+  // (At most 8 instances keep the model's choice, (4, 14, 32) for one 128x128
+  // instance: 0.4-2.3 % faster than (8, 8, 16) on two boxes.)
+  const bool prefer8 = !fG && mode == kModeBwd && layout == 2 && W == 128 && B > 8 && env_int("IRLMX_PLAN_G8", 1) != 0;
   for (int pass = prefer8 ? 0 : 1; pass < 2 && !ok; ++pass)
   for (int G = kTMax; G >= 1; --G) {
     if (fG && G != fG) continue;

@@ -2,7 +2,7 @@
 
 128x128 (configs 3 and 5): the device's backward pass (2*S = 32,768 sweeps on
 the cluster plan the planner picks for two instances -- column-strip layout,
-R = 8 / G = 8 / C = 16 tiles per instance since round 6, halo exchanges, block-boundary
+R = 4 / G = 14 / C = 32 tiles per instance, halo exchanges, block-boundary
 rescaling; the bench's own B = 64 plan is tested in test_gpu_bench_plans.py)
 and a forward pass capped at 3,000 sweeps, against the CPU oracle's sparse-operand restatement of the same
 reference statements (oracle/maxent_oracle.py ``*_csr``, maxent.py:98-112,
