@@ -77,6 +77,24 @@ def test_compaction_bit_identical_fused(dev):
     assert comp["widths"][0] == 6 and comp["widths"][1] == 5 and min(comp["widths"]) < 5
 
 
+def test_prime_compaction_leaves_state_unchanged(dev):
+    """BatchedMaxEnt.prime_compaction (run before bench.py's clocks start: it
+    loads the code of the stop test, the compaction and the working-set update)
+    runs on a scratch copy: the object's theta, step counts, activity and step
+    index are untouched, and a run after it equals a run without it bit for bit."""
+    from irlmx.batch import BatchedMaxEnt
+    mdp, e_f, p0, term = staggered_workload(dev, 16, 6)
+    plain = BatchedMaxEnt(mdp, e_f, p0, term)
+    primed = BatchedMaxEnt(mdp, e_f, p0, term)
+    theta0 = primed.theta.clone()
+    primed.prime_compaction()
+    assert torch.equal(primed.theta, theta0) and primed.k == 0 and primed._work is None
+    assert bool(primed.active.all()) and int(primed.steps.sum()) == 0
+    r1, k1 = plain.run(eps=1e-4, max_steps=4000)
+    r2, k2 = primed.run(eps=1e-4, max_steps=4000)
+    assert torch.equal(k1, k2) and torch.equal(r1, r2)
+
+
 def test_compaction_bit_identical_cluster(dev):
     """128x128 (cluster shape, the bench's grid): five instances, five gradient
     steps with instances 0 and 1 stopping early; the compacted run re-plans for
