@@ -134,6 +134,8 @@ def compare_steps(z, checked, steps, n_states, causal=False):
                 ref = z[f"{key}{name}{i}"]
                 close(vec[z[key + "idx"]] if key + "idx" in z.files else vec, ref, (b, name, i))
                 check_sums(z, f"{key}{name}{i}", vec)
+                if f"{key}{name}{i}_full" in z.files:   # whole vectors kept for some steps of subset fixtures
+                    close(vec, z[f"{key}{name}{i}_full"], (b, name, i, "whole vector"))
 
 
 def test_config3_bench_plan_three_irl_steps(dev):
@@ -158,7 +160,8 @@ def test_config4_bench_plan_irl_steps(dev):
     """Config 4: 256x256, 32 instances per GPU -- backward plan R=32 / G=4 / C=8,
     20 states per lane in column quads with compact weights (three per state),
     all 32 instances in one launch; every gradient step the fixture holds for
-    b = 0 and 31 (vectors checked on 4,096 states + whole-vector sums)."""
+    b = 0 and 31 (vectors checked on 4,096 states + whole-vector sums, and all
+    65,536 states of SVF and theta at steps 1 and 7 -- round 6)."""
     from irlmx import ops
     z, checked, mdp, steps = run_bench_workload(dev, "c4", 256, 32, fixture_steps("c4"))
     assert plan_subset(ops.execution_plan(mdp, "backward"), C4_BWD_PLAN) == C4_BWD_PLAN

@@ -17,7 +17,8 @@ irlmx.demos.sample with seed 1234 + b):
   full_c4.npz  256x256, 32 instances per GPU: b = 0 and 31, the first 7 steps
                (the bench's timed window at --steps 5 --warmup 2).
                Vectors of 65,536 states are stored on a fixed subset of 4,096
-               states plus whole-vector sums (sum, sum |x|, max |x|).
+               states plus whole-vector sums (sum, sum |x|, max |x|); the SVF
+               and theta of steps 1 and 7 also whole (svf0_full, theta6_full, ...).
   full_c5.npz  128x128 causal (config 5): the forward pass to convergence on the
                reference's own soft-VI policy (tests/golden/causal_128.npz), and
                the first 7 irl_causal steps (maxent.py:437-450) of the bench's
@@ -90,6 +91,9 @@ def bench_instance(size, b, n_total):
     return slip, mats, e_f, p0
 
 
+FULL_STEPS = {"c4": (0, 6)}   # steps (0-based) whose whole vectors are kept although S > SUBSET_MAX_S
+
+
 def job_irl(args):
     cfg, size, n_total, b, n_steps, causal = args
     t0 = time.time()
@@ -104,6 +108,9 @@ def job_irl(args):
     for i in range(n_steps):
         pack(f"svf{i}", res["svf"][i], idx, out)
         pack(f"theta{i}", res["theta"][i], idx, out)
+        if idx is not None and i in FULL_STEPS.get(cfg, ()):
+            out[f"svf{i}_full"] = res["svf"][i]
+            out[f"theta{i}_full"] = res["theta"][i]
     pi0 = res["pi"][0]
     if idx is None:
         out["pi0"] = pi0
