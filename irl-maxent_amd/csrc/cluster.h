@@ -23,7 +23,7 @@ constexpr int kSptMaxQuadBwdCW = 20;
 constexpr int kTMax = 16;          // max sweeps per block (= max ghost rows)
 constexpr int kSoloBwdT = 256;     // backward sweeps per block of a solo tile (no ghost rows)
 #ifndef IRLMX_RESCALE_EVERY
-#define IRLMX_RESCALE_EVERY 16
+#define IRLMX_RESCALE_EVERY 32
 #endif
 constexpr int kRescaleEvery = IRLMX_RESCALE_EVERY;  // backward: max blocks between rescales
 constexpr size_t kMaxLdsBytes = 160 * 1024;  // LDS per CU (one workgroup per CU)
