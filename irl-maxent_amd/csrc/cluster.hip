@@ -863,7 +863,7 @@ __global__ void __launch_bounds__(NT) cluster_kernel(ClusterArgs a) {
         }
       };
       // (the full-bookkeeping replay, rare, keeps the p0 add everywhere: one copy less of the loop)
-      if (MODE == kModeFwd && (decltype(fulltag)::value && kProof || wave_p0)) go(std::true_type{});
+      if (MODE == kModeFwd && ((decltype(fulltag)::value && kProof) || wave_p0)) go(std::true_type{});
       else go(std::false_type{});
     }
   };

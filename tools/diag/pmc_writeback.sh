@@ -1,18 +1,20 @@
 #!/bin/bash
 # L2 write-back / eviction counters of one config-3 backward dispatch
-# (tools/diag/bwd_once.py), default granule layout vs the unpadded one
-# (build/gran_pad0: IRLMX_GRAN_PAR_PAD = IRLMX_GRAN_INST_PAD = 0).  Each
-# counter set is its own rocprofv3 pass (at most 4 TCC counters per pass).
-#   tools/diag/pmc_writeback.sh [SIZE B]
+# (tools/diag/bwd_once.py), the default build vs variant builds
+# (build/<name>/libirlmx.so from tools/diag/build_variant.sh; default list:
+# gran_pad0 = IRLMX_GRAN_PAR_PAD = IRLMX_GRAN_INST_PAD = 0).  Each counter set
+# is its own rocprofv3 pass (at most 4 TCC counters per pass).
+#   VARIANTS="default resc16" tools/diag/pmc_writeback.sh [SIZE B [OUTDIR]]
 ROOT=$(pwd)
-OUT=$ROOT/gpurun_out/pmc_wb
+OUT=$ROOT/gpurun_out/${3:-pmc_wb}
+VARIANTS=${VARIANTS:-default gran_pad0}
 mkdir -p $OUT
 export TMPDIR=/tmp
 ARGS="${1:-128} ${2:-64}"
 i=0
-for v in default pad0; do
+for v in $VARIANTS; do
   lib=""
-  [ $v = pad0 ] && lib=$ROOT/build/gran_pad0/libirlmx.so
+  [ $v != default ] && lib=$ROOT/build/$v/libirlmx.so
   for set in "TCC_NORMAL_WRITEBACK_sum TCC_ALL_TC_OP_WB_WRITEBACK_sum TCC_NORMAL_EVICT_sum TCC_PROBE_EVICT_sum" \
              "TCC_EA0_WRREQ_sum TCC_EA0_WRREQ_64B_sum TCC_EA0_WRREQ_DRAM_sum TCC_WRITE_sum" \
              "TCC_HIT_sum TCC_MISS_sum TCC_STREAMING_REQ_sum TCC_ALL_TC_OP_INV_EVICT_sum"; do
@@ -23,10 +25,10 @@ for v in default pad0; do
     [ $rc -ne 0 ] && tail -5 $OUT/${v}_p$i.log && exit $rc
   done
 done
-python3 - "$OUT" <<'PY'
+python3 - "$OUT" $VARIANTS <<'PY'
 import csv, glob, sys, collections
 out = sys.argv[1]
-for v in ("default", "pad0"):
+for v in sys.argv[2:]:
     vals = {}
     for path in glob.glob(f"{out}/{v}_p*/**/*counter_collection.csv", recursive=True):
         rows = [r for r in csv.DictReader(open(path)) if "cluster_kernel<1" in r["Kernel_Name"]]
