@@ -148,6 +148,17 @@ int64_t irlmx_device_check_failures(void);
 #define IRLMX_PROP_ELL_SORTED 0x2
 int irlmx_mdp_properties(const irlmx_mdp* mdp, int32_t* props, void* stream);
 
+/*
+ * numpy's float64 exp / log as the kernels evaluate them (np_exp / np_log in
+ * csrc/common.h: the soft VI softmax, maxent.py:260-276, and its policy,
+ * maxent.py:341; diagnostics and parity tests, no reference counterpart):
+ * y[i] = f(x[i]) for 0 <= i < n on device pointers, asynchronous on `stream`.
+ * op IRLMX_NPMATH_EXP or IRLMX_NPMATH_LOG; n = 0 is a no-op.
+ */
+#define IRLMX_NPMATH_EXP 0
+#define IRLMX_NPMATH_LOG 1
+int irlmx_numpy_math(int32_t op, const double* x, double* y, int64_t n, void* stream);
+
 /* Bytes of device workspace `op` needs for this model (0 is a valid answer). */
 size_t irlmx_workspace_bytes(const irlmx_mdp* mdp, int32_t op);
 

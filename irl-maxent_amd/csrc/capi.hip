@@ -40,6 +40,11 @@ void note_exchange_timeout(const char* shape) {
             "on the per-sweep shape (counter rerun_timeout; IRLMX_STRICT_EXCHANGE=1 makes it an error)\n", shape);
 }
 
+__global__ void numpy_math_kernel(int op, const double* __restrict__ x, double* __restrict__ y, int64_t n) {
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
+    y[i] = op == IRLMX_NPMATH_EXP ? np_exp(x[i]) : np_log(x[i]);
+}
+
 static std::vector<DcheckTake>& dcheck_registry() {
   static std::vector<DcheckTake> r;
   return r;
@@ -63,6 +68,26 @@ extern "C" int64_t irlmx_device_check_failures(void) {
 }
 
 extern "C" int irlmx_abi_version(void) { return IRLMX_ABI_VERSION; }
+
+extern "C" int irlmx_numpy_math(int32_t op, const double* x, double* y, int64_t n, void* stream) {
+  if (op != IRLMX_NPMATH_EXP && op != IRLMX_NPMATH_LOG) {
+    irlmx::set_error("unknown op %d", op);
+    return IRLMX_EINVAL;
+  }
+  if (n < 0) {
+    irlmx::set_error("n = %lld < 0", (long long)n);
+    return IRLMX_EINVAL;
+  }
+  if (n == 0) return IRLMX_OK;
+  if (!x || !y) {
+    irlmx::set_error("x or y is NULL");
+    return IRLMX_EINVAL;
+  }
+  const int64_t blocks = (n + 255) / 256 < 4096 ? (n + 255) / 256 : 4096;
+  hipLaunchKernelGGL(irlmx::numpy_math_kernel, dim3((unsigned)blocks), dim3(256), 0, (hipStream_t)stream, op, x, y, n);
+  if (hipError_t e = hipGetLastError(); e != hipSuccess) return irlmx::hip_fail(e, "numpy_math_kernel");
+  return IRLMX_OK;
+}
 
 extern "C" const char* irlmx_last_error(void) { return irlmx::g_err; }
 

@@ -413,7 +413,7 @@ dense_bellman_finish_kernel(DenseView d, DenseBellman a, DenseBufs w) {
       for (int act = 0; act < A; ++act) {
         const double dot = wave_dot(Pb + ((size_t)act * S + s) * S, v, S, lane);
         const double q = __dadd_rn(r, __dmul_rn(a.discount, dot));
-        if (lane == 0) a.pi[((size_t)b * S + s) * A + act] = exp(q - vn);
+        if (lane == 0) a.pi[((size_t)b * S + s) * A + act] = np_exp(q - vn);
       }
     }
   }

@@ -545,7 +545,7 @@ __global__ void __launch_bounds__(kDG) dense_bellman_grid_kernel(DenseGridArgs a
   if (owner) {
     if (a.value) a.value[srow] = vkeep;
     if (SOFT)
-      for (int act = 0; act < A; ++act) a.out[srow * A + act] = exp(qkeep[act] - vkeep);  // maxent.py:341
+      for (int act = 0; act < A; ++act) a.out[srow * A + act] = np_exp(qkeep[act] - vkeep);  // maxent.py:341
   }
   if (blk == 0 && tid == 0) {
     if (a.iters) a.iters[b] = k;

@@ -1215,7 +1215,7 @@ __device__ inline void soft_policy_row(const SoftArgs& a, int b, int s, const in
       for (int k = 0; k < m.K; ++k) dot = fma(row_val(m, b, act, k, s), vold[row_nbr(m, b, s, k)], dot);
     }
     const double q = __dadd_rn(r, __dmul_rn(a.discount, dot));
-    a.pi[((size_t)b * m.S + s) * m.A + act] = exp(q - vnew);  // maxent.py:341
+    a.pi[((size_t)b * m.S + s) * m.A + act] = np_exp(q - vnew);  // maxent.py:341
   }
 }
 
@@ -1366,7 +1366,7 @@ __global__ void __launch_bounds__(1024) bellman_numpy_order_kernel(SoftArgs a) {
     if (SOFT)
       for (int act = 0; act < A; ++act) {
         const double q = __dadd_rn(rw[s], __dmul_rn(a.discount, np_row_dot<LAYOUT>(m, b, act, s, vold)));
-        a.pi[((size_t)b * S + s) * A + act] = exp(q - vnew[s]);  // maxent.py:341
+        a.pi[((size_t)b * S + s) * A + act] = np_exp(q - vnew[s]);  // maxent.py:341
       }
   }
   if (tid == 0) {
@@ -1465,7 +1465,7 @@ __global__ void __launch_bounds__(kNpCachedThreads) bellman_numpy_order_cached_k
       for (int act = 0; act < kNpCachedMaxActions; ++act) {
         if (act >= A) break;
         const double q = __dadd_rn(rr[j], __dmul_rn(a.discount, rows.dot(j, act, s < m1, x)));
-        a.pi[((size_t)b * S + s) * A + act] = exp(q - vnew[s]);  // maxent.py:341
+        a.pi[((size_t)b * S + s) * A + act] = np_exp(q - vnew[s]);  // maxent.py:341
       }
     }
   }
@@ -1869,7 +1869,7 @@ __global__ void __launch_bounds__(kGridThreads) bellman_grid_kernel(SoftArgs a, 
     const size_t o = (size_t)b * S + sidx[j];
     if (a.value) a.value[o] = cur[j];
     if (SOFT)
-      for (int act = 0; act < A; ++act) a.pi[o * A + act] = exp(q[j][act] - cur[j]);  // maxent.py:341
+      for (int act = 0; act < A; ++act) a.pi[o * A + act] = np_exp(q[j][act] - cur[j]);  // maxent.py:341
   }
   if (blk == 0 && tid == 0) {
     if (a.iters) a.iters[b] = k;

@@ -70,6 +70,7 @@ SIGNATURES = {
     "irlmx_counters": (ctypes.c_int, [_P, _I32]),
     "irlmx_workspace_bytes": (_SZ, [_MDP, _I32]),
     "irlmx_mdp_properties": (ctypes.c_int, [_MDP, _P, _P]),
+    "irlmx_numpy_math": (ctypes.c_int, [ctypes.c_int32, _P, _P, ctypes.c_int64, _P]),
     "irlmx_device_checks_enabled": (ctypes.c_int, []),
     "irlmx_device_check_failures": (_I64, []),
     "irlmx_backward_maxent": (ctypes.c_int, [_MDP, _P, _P, _I32, _P, _P, _P, _SZ, _P]),

@@ -33,6 +33,7 @@
 #include <stddef.h>
 #include <stdint.h>
 #include <stdlib.h>
+#include <string.h>
 
 #define NBMAX 2048
 
@@ -291,4 +292,106 @@ int blas_order_backward_maxent_csr(const int64_t* indptr, const int32_t* indices
     for (int a = 0; a < A; ++a) pi[(size_t)s * A + a] = za[(size_t)s * A + a] / zs[s];
   free(zs); free(dot); free(za);
   return 0;
+}
+
+/*
+ * TEST INFRASTRUCTURE (oracle).  np.exp / np.log for float64 as numpy 2.2.6
+ * computes them on an AVX512_SKX host: the contiguous loops
+ * DOUBLE_exp_AVX512_SKX / DOUBLE_log_AVX512_SKX call SVML's __svml_exp8_ha /
+ * __svml_log8_ha (numpy's vendored SVML, no source in this image).  Restated
+ * from their instruction sequence (constants as stored in numpy's rodata),
+ * one scalar lane at a time, with the two non-portable steps replaced by exact
+ * equivalents:
+ *   exp: the {rz-sae} fma x / ln2 + shifter -- round to nearest, then step
+ *        down one grid point (1/16) when the exact residual is negative;
+ *   log: vrcp14pd + vrndscalepd(0x58) of the mantissa -- rcp14 reads the top
+ *        16 mantissa bits u only, and the rounded result R = (32 - n) / 32
+ *        with n = #{t : u >= t} over 16 thresholds found by evaluating the
+ *        instruction for all 65,536 u (tools/gen_npmath.py).
+ * Inputs SVML sends to its scalar rare path (exp: |x| >= 707.70, NaN; log:
+ * x <= 0, inf, NaN) use libm here.  The device twins are np_exp / np_log in
+ * irl-maxent_amd/csrc/common.h; both are pinned against np.exp / np.log
+ * (tests/golden/npmath.npz, tests/test_npmath.py, tests/test_gpu_npmath.py).
+ */
+static const double kExpT0[16] = {
+    0x1.0000000000000p+0, 0x1.0b5586cf9890fp+0, 0x1.172b83c7d517bp+0, 0x1.2387a6e756238p+0,
+    0x1.306fe0a31b715p+0, 0x1.3dea64c123422p+0, 0x1.4bfdad5362a27p+0, 0x1.5ab07dd485429p+0,
+    0x1.6a09e667f3bcdp+0, 0x1.7a11473eb0187p+0, 0x1.8ace5422aa0dbp+0, 0x1.9c49182a3f090p+0,
+    0x1.ae89f995ad3adp+0, 0x1.c199bdd85529cp+0, 0x1.d5818dcfba487p+0, 0x1.ea4afa2a490dap+0};
+static const double kExpT1[16] = {
+    0x0.0p+0, 0x1.79aa65d837b6dp-54, -0x1.01b15eaa59348p-55, 0x1.68efde3a8a894p-54,
+    0x1.34d754db0abb6p-55, 0x1.59f48a72a4c6dp-55, 0x1.690cebb7aafb0p-56, 0x1.063e1e21c5409p-54,
+    -0x1.3b3efbf5e2228p-54, -0x1.b32dcb94da51dp-56, 0x1.db72fc1f0eab4p-55, 0x1.1affc2b91ce27p-56,
+    0x1.c1a7792cb3387p-55, 0x1.36eae30af0cb3p-56, 0x1.4a385a63d07a7p-56, -0x1.ff7128fd391f0p-55};
+static const double kLogTH[16] = {
+    0x0.0p+0, -0x1.f0a30c0120000p-5, -0x1.e27076e2b0000p-4, -0x1.5ff3070a78000p-3,
+    -0x1.c8ff7c79a8000p-3, -0x1.1675cababc000p-2, -0x1.4618bc21c4000p-2, -0x1.739d7f6bbc000p-2,
+    0x1.269621134c000p-2, 0x1.f991c6cb38000p-3, 0x1.a93ed3c8b0000p-3, 0x1.5bf406b540000p-3,
+    0x1.1178e82280000p-3, 0x1.9335e5d590000p-4, 0x1.08598b59e0000p-4, 0x1.0415d89e80000p-5};
+static const double kLogTL[16] = {
+    0x0.0p+0, 0x1.3ab33d066d1d2p-42, 0x1.a342c2af0003cp-45, -0x1.3d3c873e20a07p-43,
+    -0x1.a21ac25d81ef3p-43, 0x1.9f1fc63382a8fp-42, -0x1.ec27d0b7b37b3p-42, -0x1.0069ce24c53fbp-42,
+    0x1.b92783beb7677p-42, 0x1.9bcbecca0cdf3p-42, -0x1.30e486a0ac42dp-42, 0x1.ed8fdc149767ep-42,
+    -0x1.b8421cc74be04p-43, 0x1.2622b8757a8fbp-42, 0x1.d034451fecdfbp-43, -0x1.77771fd187145p-42};
+static const unsigned kRcpSteps[16] = {1039u, 3223u, 5556u, 8048u, 10726u, 13603u, 16707u, 20063u,
+                                       23705u, 27669u, 32007u, 36764u, 42010u, 47824u, 54300u, 61568u};
+
+static double np_exp1(double x) {
+  if (!(fabs(x) < 0x1.61da04cbafe44p+9)) return exp(x);
+  const double shift = 0x1.8000000003ff0p+48, inv_ln2 = 0x1.71547652b82fep+0;
+  double xs = fma(x, inv_ln2, shift);
+  if (fma(x, inv_ln2, shift - xs) < 0.0) xs -= 0x1p-4;
+  const double n = xs - shift;
+  uint64_t bits;
+  memcpy(&bits, &xs, 8);
+  const int j = (int)(bits & 15);
+  double r = fma(-n, 0x1.62e42fefa39efp-1, x);
+  r = fma(-0x1.abc9e3b39803fp-56, n, r);
+  const double r2 = r * r;
+  const double a = fma(r, 0x1.7411836940c04p-10, 0x1.1101cbbc265c0p-7);
+  const double b = fma(r, 0x1.55557242d68fep-5, 0x1.5555553939732p-3);
+  const double c = fma(r, 0x1.000000000d008p-1, 0x1.fffffffffff70p-1);
+  double p = fma(r2, a, b);
+  p = fma(r2, p, c);
+  double q = fma(p, r, kExpT1[j]);
+  q = fma(kExpT0[j], q, kExpT0[j]);
+  return ldexp(q, (int)floor(n));
+}
+
+static double np_log1(double x) {
+  if (!(x > 0.0) || isinf(x)) return log(x);
+  int e;
+  const double m = ldexp(frexp(x, &e), 1);
+  double E = (double)(e - 1);
+  uint64_t bits;
+  memcpy(&bits, &m, 8);
+  const unsigned u = (unsigned)(bits >> 36) & 0xffffu;
+  int nd = 0;
+  for (int i = 0; i < 16; ++i) nd += u >= kRcpSteps[i];
+  const double R = (double)(32 - nd) * 0x1p-5;
+  const double r = fma(R, m, -1.0);
+  if (nd > 8) E += 1.0;
+  const int idx = (16 - nd) & 15;
+  const double p1 = fma(r, 0x1.249229cee81efp-3, -0x1.55553fb28db06p-3);
+  double p2 = fma(r, 0x1.c81cd309d7c70p-4, -0x1.007357e93af62p-3);
+  const double r2 = r * r;
+  double p3 = fma(r, 0x1.9999999cc9f5cp-3, -0x1.00000000c05bdp-2);
+  p2 = fma(r2, p2, p1);
+  const double r4 = r2 * r2;
+  const double p4 = fma(r, 0x1.5555555555466p-2, -0x1.fffffffffffc6p-2);
+  p3 = fma(r2, p3, p4);
+  const double hi = fma(E, 0x1.62e42fefa0000p-1, kLogTH[idx]);
+  p2 = fma(r4, p2, p3);
+  const double s = hi + r;
+  const double rl = r - (s - hi);
+  p2 = fma(r2, p2, rl);
+  const double lo = fma(0x1.cf79abc9e0000p-40, E, kLogTL[idx]);
+  return s + (p2 + lo);
+}
+
+void numpy_exp_restated(const double* x, double* y, long long n) {
+  for (long long i = 0; i < n; ++i) y[i] = np_exp1(x[i]);
+}
+void numpy_log_restated(const double* x, double* y, long long n) {
+  for (long long i = 0; i < n; ++i) y[i] = np_log1(x[i]);
 }

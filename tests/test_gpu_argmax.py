@@ -193,19 +193,18 @@ def test_numpy_order_generic_and_batched(dev):
 
 def test_causal_policy_argmax(dev):
     """The drop-in local_causal_action_probabilities sums every P_a . v in numpy's
-    order (irlmx_soft_backward_numpy_order), so the policy's mirror-symmetric
-    ties (diagonal states of the unit-reward cases, decided in the last bit by
-    that order) fall as the reference's do: argmax identical at every pinned
-    case, sweep counts identical, values within 1e-9.  (exp / log are the
-    device's: the reference's own bits change with numpy's SIMD exp / log --
-    NPY_DISABLE_CPU_FEATURES=AVX512F gives other bits, the same argmax.)"""
+    order (irlmx_soft_backward_numpy_order) and evaluates exp / log as numpy's
+    AVX512_SKX loops do (np_exp / np_log, csrc/common.h), so the policy is
+    bit-identical to the reference's output -- the mirror-symmetric ties of the
+    unit-reward cases, decided in the last bit, included -- with identical sweep
+    counts, on every layout."""
     import maxent as M
     from irlmx import DeviceMDP, ops
     for name, P, term, r, g, ref in _pinned_causal_cases():
         pi = M.local_causal_action_probabilities(P, term, r, g)
+        assert np.array_equal(pi, ref), (name, np.max(np.abs(pi - ref)), int((pi != ref).sum()))
         got, want = np.argmax(pi, axis=1), np.argmax(ref, axis=1)
         assert np.array_equal(got, want), (name, _argmax_report(got, want))
-        assert np.max(np.abs(pi - ref)) <= 1e-9 * np.max(np.abs(ref)), name
         _, _, ks_ref = O.soft_backward(P, term, r, g)
         for layout in ("stencil", "ell", "dense"):
             mdp = DeviceMDP.from_dense(P, device=dev, layout=layout)
@@ -297,8 +296,8 @@ def test_config1_irl_bit_identical(dev):
     """BASELINE config 1 (src/main.py) through the drop-in: maxent.irl's 375
     steps reproduce the reference's recovered reward bit for bit (backward and
     forward in numpy's order, the caller's numpy optimiser on the host), and
-    irl_causal its 419 steps within 1e-9 (the soft VI's exp / log are the
-    device's)."""
+    irl_causal its 419 steps too (soft VI with numpy's exp / log, np_exp /
+    np_log)."""
     import maxent as M
     from conftest import unpack_trajectories
     z = load_golden("config1")
@@ -310,7 +309,7 @@ def test_config1_irl_bit_identical(dev):
     opt = O.ExpSga(lr=O.linear_decay(0.2))
     r = M.irl_causal(z["p_transition"], np.identity(25), [24], tjs, opt, O.Constant(1.0), 0.7)
     assert opt.k == int(z["causal_steps"]) == 419
-    assert np.max(np.abs(r - z["reward_causal"])) <= 1e-9
+    assert np.array_equal(r, z["reward_causal"]), np.max(np.abs(r - z["reward_causal"]))
 
 
 @pytest.mark.parametrize("size", [23, 31, 32])
@@ -379,9 +378,6 @@ def test_backward_numpy_order_64x64_against_restatement(dev, monkeypatch):
     assert np.array_equal(np.argmax(got, axis=1), np.argmax(ref, axis=1))
 
 
-NEAR_TIE = 1e-14   # relative top-two gap below which a soft-VI policy state counts as tied
-
-
 class IcyWorld64:
     """The reference IcyGridWorld(64, 0.2) API the solver drop-ins use: size,
     actions, n_states / n_actions, state_index_transition, p_transition (the
@@ -409,12 +405,10 @@ def test_config2_drop_ins_against_reference(dev):
       solver.optimal_policy_from_value and solver.optimal_policy
       (solver.py:107-152): np.array_equal with the reference's greedy policy.
     * maxent.local_causal_action_probabilities (maxent.py:279-341): soft-VI
-      sweep count identical, policy within 1e-9, argmax identical at every
-      state the reference does not tie within a few ulps; at theta = 1, whose
-      ~2,200 mirror-symmetric near-ties (710 exact) are decided by the last bits
-      of exp / log (the device's own, not numpy's AVX-512 ones), the device's
-      action is one of the reference's tied best actions (measured: equal to the
-      reference's at all but 2 of them at discount 0.7)."""
+      sweep count identical, policy bit-identical (numpy's order for P_a . v,
+      numpy's exp / log: np_exp / np_log), so np.array_equal argmax -- at
+      theta = 1 too, whose ~2,200 mirror-symmetric near-ties (710 exact) are
+      decided by the last bits of ~700 sweeps of exp / log."""
     import maxent as M
     import solver as S
     from irlmx import ops
@@ -433,25 +427,14 @@ def test_config2_drop_ins_against_reference(dev):
             ref = z[c + "__pi"]
             pi = M.local_causal_action_probabilities(P, [n - 1], r, g)
             got, want = np.argmax(pi, axis=1), np.argmax(ref, axis=1)
-            # States whose best two actions the reference separates by at most
-            # NEAR_TIE (relative: a few ulps) are ties decided by the last bits of
-            # ~700 sweeps of exp / log, which the device computes with its own
-            # functions (numpy's AVX-512 exp / log and glibc's log near 1 are not
-            # restated): there the device's action must be one of the reference's
-            # near-tied best actions.  Everywhere else: the reference's argmax.
-            top = np.sort(ref, axis=1)
-            near = (top[:, -1] - top[:, -2]) <= NEAR_TIE * top[:, -1]
-            bad = np.flatnonzero((got != want) & ~near)
-            assert bad.size == 0, (c, _argmax_report(got, want))
-            tied_ok = ref[np.arange(n), got] >= top[:, -1] * (1.0 - NEAR_TIE)
-            assert tied_ok.all(), (c, "argmax outside the near-tied set at", np.flatnonzero(~tied_ok)[:8])
-            assert np.max(np.abs(pi - ref)) <= 1e-9 * np.max(np.abs(ref)), c
+            assert np.array_equal(pi, ref), (c, np.max(np.abs(pi - ref)), int((pi != ref).sum()))
+            assert np.array_equal(got, want), (c, _argmax_report(got, want))
             _, _, ks, st = ops.soft_backward(mdp, r, O.terminal_reward([n - 1], n), g, numpy_order=True)
             assert int(ks[0]) == int(z[c + "__k_s"]) and int(st[0]) == 0, (c, int(ks[0]))
-            print(f"[c2_64] {c}: {int(ks[0])} sweeps; argmax equal at all {int((~near).sum())} states not tied "
-                  f"within {NEAR_TIE:g}; at the {int(near.sum())} near-tied states equal at "
-                  f"{int(near.sum()) - int(((got != want) & near).sum())}, the rest one of the tied best actions; "
-                  f"max |pi - ref| {np.max(np.abs(pi - ref)):.2e}", flush=True)
+            top = np.sort(ref, axis=1)
+            near = int(((top[:, -1] - top[:, -2]) <= 1e-14 * top[:, -1]).sum())
+            print(f"[c2_64] {c}: {int(ks[0])} sweeps; policy bit-identical, argmax equal at all {n} states "
+                  f"({near} of them tied within 1e-14)", flush=True)
             continue
         avg = bool(z[c + "__average"])
         fn = S.stochastic_value_iteration if avg else S.value_iteration
