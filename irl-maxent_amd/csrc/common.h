@@ -95,17 +95,44 @@ __device__ inline double np_minimum(double a, double b) {
 // |x| >= 707.7, NaN; log: x <= 0, inf, NaN) uses ocml, which agrees with it
 // except in the last bit of some results below 1e-307 or above 1e307.
 // ---------------------------------------------------------------------------
-__device__ inline double np_exp(double x) {
-  // 2^(j/16) as a double (kT0) and its rounding error (kT1)
-  constexpr double kT0[16] = {0x1.0000000000000p+0, 0x1.0b5586cf9890fp+0, 0x1.172b83c7d517bp+0, 0x1.2387a6e756238p+0,
-                              0x1.306fe0a31b715p+0, 0x1.3dea64c123422p+0, 0x1.4bfdad5362a27p+0, 0x1.5ab07dd485429p+0,
-                              0x1.6a09e667f3bcdp+0, 0x1.7a11473eb0187p+0, 0x1.8ace5422aa0dbp+0, 0x1.9c49182a3f090p+0,
-                              0x1.ae89f995ad3adp+0, 0x1.c199bdd85529cp+0, 0x1.d5818dcfba487p+0, 0x1.ea4afa2a490dap+0};
-  constexpr double kT1[16] = {0x0.0p+0, 0x1.79aa65d837b6dp-54, -0x1.01b15eaa59348p-55, 0x1.68efde3a8a894p-54,
-                              0x1.34d754db0abb6p-55, 0x1.59f48a72a4c6dp-55, 0x1.690cebb7aafb0p-56, 0x1.063e1e21c5409p-54,
-                              -0x1.3b3efbf5e2228p-54, -0x1.b32dcb94da51dp-56, 0x1.db72fc1f0eab4p-55, 0x1.1affc2b91ce27p-56,
-                              0x1.c1a7792cb3387p-55, 0x1.36eae30af0cb3p-56, 0x1.4a385a63d07a7p-56, -0x1.ff7128fd391f0p-55};
-  if (!(fabs(x) < 0x1.61da04cbafe44p+9)) return exp(x);  // rare path
+// The four 16-entry tables in one array (kernels with a hot soft-VI loop stage
+// it in LDS, np_stage_tables, and pass that copy: a divergent table read is then
+// an LDS read instead of a global one on the sweep's dependency chain):
+//   [0, 16)  exp: 2^(j/16) as a double       [16, 32) exp: its rounding error
+//   [32, 48) log: -log(R) high part          [48, 64) log: -log(R) low part
+// for the 5-bit reciprocal R of the mantissa, indexed by R's top four mantissa
+// bits (R < 0.75 folds a factor 2 into the exponent).
+constexpr int kNpTabLen = 64;
+static __constant__ double kNpTab[kNpTabLen] = {
+    0x1.0000000000000p+0, 0x1.0b5586cf9890fp+0, 0x1.172b83c7d517bp+0, 0x1.2387a6e756238p+0,
+    0x1.306fe0a31b715p+0, 0x1.3dea64c123422p+0, 0x1.4bfdad5362a27p+0, 0x1.5ab07dd485429p+0,
+    0x1.6a09e667f3bcdp+0, 0x1.7a11473eb0187p+0, 0x1.8ace5422aa0dbp+0, 0x1.9c49182a3f090p+0,
+    0x1.ae89f995ad3adp+0, 0x1.c199bdd85529cp+0, 0x1.d5818dcfba487p+0, 0x1.ea4afa2a490dap+0,
+    0x0.0p+0, 0x1.79aa65d837b6dp-54, -0x1.01b15eaa59348p-55, 0x1.68efde3a8a894p-54,
+    0x1.34d754db0abb6p-55, 0x1.59f48a72a4c6dp-55, 0x1.690cebb7aafb0p-56, 0x1.063e1e21c5409p-54,
+    -0x1.3b3efbf5e2228p-54, -0x1.b32dcb94da51dp-56, 0x1.db72fc1f0eab4p-55, 0x1.1affc2b91ce27p-56,
+    0x1.c1a7792cb3387p-55, 0x1.36eae30af0cb3p-56, 0x1.4a385a63d07a7p-56, -0x1.ff7128fd391f0p-55,
+    0x0.0p+0, -0x1.f0a30c0120000p-5, -0x1.e27076e2b0000p-4, -0x1.5ff3070a78000p-3,
+    -0x1.c8ff7c79a8000p-3, -0x1.1675cababc000p-2, -0x1.4618bc21c4000p-2, -0x1.739d7f6bbc000p-2,
+    0x1.269621134c000p-2, 0x1.f991c6cb38000p-3, 0x1.a93ed3c8b0000p-3, 0x1.5bf406b540000p-3,
+    0x1.1178e82280000p-3, 0x1.9335e5d590000p-4, 0x1.08598b59e0000p-4, 0x1.0415d89e80000p-5,
+    0x0.0p+0, 0x1.3ab33d066d1d2p-42, 0x1.a342c2af0003cp-45, -0x1.3d3c873e20a07p-43,
+    -0x1.a21ac25d81ef3p-43, 0x1.9f1fc63382a8fp-42, -0x1.ec27d0b7b37b3p-42, -0x1.0069ce24c53fbp-42,
+    0x1.b92783beb7677p-42, 0x1.9bcbecca0cdf3p-42, -0x1.30e486a0ac42dp-42, 0x1.ed8fdc149767ep-42,
+    -0x1.b8421cc74be04p-43, 0x1.2622b8757a8fbp-42, 0x1.d034451fecdfbp-43, -0x1.77771fd187145p-42};
+
+// Copy the tables into the workgroup's LDS array `t` (threads 0..63; the caller
+// synchronises before the first use).
+__device__ inline void np_stage_tables(double* t) {
+  if (threadIdx.x < kNpTabLen) t[threadIdx.x] = kNpTab[threadIdx.x];
+}
+
+__device__ inline double np_exp(double x, const double* t = kNpTab) {
+  if (!(fabs(x) < 0x1.61da04cbafe44p+9)) {  // SVML's rare path
+    if (x <= -746.0) return 0.0;            // underflow (-inf: soft VI's first softmax of a non-terminal state)
+    if (x >= 710.0) return (double)INFINITY;
+    return exp(x);                          // NaN, and the subnormal / near-overflow results
+  }
   // xs = x / ln2 + shifter rounded toward zero to a multiple of 1/16 (SVML's
   // {rz-sae} fma): the round-to-nearest fma, stepped down one grid point when
   // it rounded up (the sign of the exact residual x / ln2 - N decides).
@@ -114,6 +141,7 @@ __device__ inline double np_exp(double x) {
   if (__fma_rn(x, kInvLn2, kShift - xs) < 0.0) xs -= 0x1p-4;
   const double n = xs - kShift;  // k / 16, exact
   const int j = (int)(__double_as_longlong(xs) & 15);
+  const double t0 = t[j], t1 = t[16 + j];
   double r = __fma_rn(-n, 0x1.62e42fefa39efp-1, x);
   r = __fma_rn(-0x1.abc9e3b39803fp-56, n, r);
   const double r2 = __dmul_rn(r, r);
@@ -122,37 +150,31 @@ __device__ inline double np_exp(double x) {
   const double c = __fma_rn(r, 0x1.000000000d008p-1, 0x1.fffffffffff70p-1);
   double p = __fma_rn(r2, a, b);
   p = __fma_rn(r2, p, c);
-  double q = __fma_rn(p, r, kT1[j]);
-  q = __fma_rn(kT0[j], q, kT0[j]);
+  double q = __fma_rn(p, r, t1);
+  q = __fma_rn(t0, q, t0);
   return ldexp(q, (int)floor(n));
 }
 
-__device__ inline double np_log(double x) {
-  // -log(R) for the 5-bit reciprocal R of the mantissa, index = R's top four
-  // mantissa bits (R < 0.75 folds a factor 2 into the exponent), hi / lo parts
-  constexpr double kTH[16] = {0x0.0p+0, -0x1.f0a30c0120000p-5, -0x1.e27076e2b0000p-4, -0x1.5ff3070a78000p-3,
-                              -0x1.c8ff7c79a8000p-3, -0x1.1675cababc000p-2, -0x1.4618bc21c4000p-2, -0x1.739d7f6bbc000p-2,
-                              0x1.269621134c000p-2, 0x1.f991c6cb38000p-3, 0x1.a93ed3c8b0000p-3, 0x1.5bf406b540000p-3,
-                              0x1.1178e82280000p-3, 0x1.9335e5d590000p-4, 0x1.08598b59e0000p-4, 0x1.0415d89e80000p-5};
-  constexpr double kTL[16] = {0x0.0p+0, 0x1.3ab33d066d1d2p-42, 0x1.a342c2af0003cp-45, -0x1.3d3c873e20a07p-43,
-                              -0x1.a21ac25d81ef3p-43, 0x1.9f1fc63382a8fp-42, -0x1.ec27d0b7b37b3p-42, -0x1.0069ce24c53fbp-42,
-                              0x1.b92783beb7677p-42, 0x1.9bcbecca0cdf3p-42, -0x1.30e486a0ac42dp-42, 0x1.ed8fdc149767ep-42,
-                              -0x1.b8421cc74be04p-43, 0x1.2622b8757a8fbp-42, 0x1.d034451fecdfbp-43, -0x1.77771fd187145p-42};
+__device__ inline double np_log(double x, const double* t = kNpTab) {
   if (!(x > 0.0) || isinf(x)) return log(x);  // rare path: 0, negative, inf, NaN
   int e;
   const double m = ldexp(frexp(x, &e), 1);  // [1, 2): getmant; e - 1 = getexp
   double E = (double)(e - 1);
   // R = round-to-1/32(rcp14(m)).  rcp14 reads the top 16 mantissa bits u; the
   // rounded result falls by 1/32 at each of these u (measured exhaustively over
-  // all 65,536 u on an AVX-512 host: tools/gen_npmath.py).
+  // all 65,536 u on an AVX-512 host: tools/gen_npmath.py).  Summed as a tree
+  // (independent compares, three levels of adds): it is on the dependency chain.
   const unsigned u = (unsigned)(__double_as_longlong(m) >> 36) & 0xffffu;
-  const int nd = (u >= 1039u) + (u >= 3223u) + (u >= 5556u) + (u >= 8048u) + (u >= 10726u) + (u >= 13603u) +
-                 (u >= 16707u) + (u >= 20063u) + (u >= 23705u) + (u >= 27669u) + (u >= 32007u) + (u >= 36764u) +
-                 (u >= 42010u) + (u >= 47824u) + (u >= 54300u) + (u >= 61568u);
+  const int n0 = ((u >= 1039u) + (u >= 3223u)) + ((u >= 5556u) + (u >= 8048u));
+  const int n1 = ((u >= 10726u) + (u >= 13603u)) + ((u >= 16707u) + (u >= 20063u));
+  const int n2 = ((u >= 23705u) + (u >= 27669u)) + ((u >= 32007u) + (u >= 36764u));
+  const int n3 = ((u >= 42010u) + (u >= 47824u)) + ((u >= 54300u) + (u >= 61568u));
+  const int nd = (n0 + n1) + (n2 + n3);
+  const int idx = (16 - nd) & 15;
+  const double th = t[32 + idx], tl = t[48 + idx];
   const double R = (double)(32 - nd) * 0x1p-5;
   const double r = __fma_rn(R, m, -1.0);
   if (nd > 8) E += 1.0;
-  const int idx = (16 - nd) & 15;
   const double p1 = __fma_rn(r, 0x1.249229cee81efp-3, -0x1.55553fb28db06p-3);
   double p2 = __fma_rn(r, 0x1.c81cd309d7c70p-4, -0x1.007357e93af62p-3);
   const double r2 = __dmul_rn(r, r);
@@ -161,22 +183,22 @@ __device__ inline double np_log(double x) {
   const double r4 = __dmul_rn(r2, r2);
   const double p4 = __fma_rn(r, 0x1.5555555555466p-2, -0x1.fffffffffffc6p-2);
   p3 = __fma_rn(r2, p3, p4);
-  const double hi = __fma_rn(E, 0x1.62e42fefa0000p-1, kTH[idx]);
+  const double hi = __fma_rn(E, 0x1.62e42fefa0000p-1, th);
   p2 = __fma_rn(r4, p2, p3);
   const double s = __dadd_rn(hi, r);
   const double rl = __dsub_rn(r, __dsub_rn(s, hi));
   p2 = __fma_rn(r2, p2, rl);
-  const double lo = __fma_rn(0x1.cf79abc9e0000p-40, E, kTL[idx]);
+  const double lo = __fma_rn(0x1.cf79abc9e0000p-40, E, tl);
   return __dadd_rn(s, __dadd_rn(p2, lo));
 }
 
 // maxent.py:260-276 -- max + log(1 + exp(min - max)) with numpy's exp / log;
 // the log(1+exp) form (not log1p) is kept deliberately so rounding follows
 // the reference.
-__device__ inline double softmax2(double x1, double x2) {
+__device__ inline double softmax2(double x1, double x2, const double* t = kNpTab) {
   const double hi = np_maximum(x1, x2);
   const double lo = np_minimum(x1, x2);
-  return __dadd_rn(hi, np_log(__dadd_rn(1.0, np_exp(__dsub_rn(lo, hi)))));
+  return __dadd_rn(hi, np_log(__dadd_rn(1.0, np_exp(__dsub_rn(lo, hi), t)), t));
 }
 
 // ---------------------------------------------------------------------------

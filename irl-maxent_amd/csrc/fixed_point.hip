@@ -1316,6 +1316,7 @@ __global__ void __launch_bounds__(1024) bellman_numpy_order_kernel(SoftArgs a) {
   const Model& m = a.m;
   const int S = m.S, A = m.A;
   const int b = blockIdx.x, tid = threadIdx.x, nt = blockDim.x;
+  __shared__ double npt[kNpTabLen];
   double* const buf0 = (double*)smem;  // (two named LDS pointers, not an array: ds_* accesses, not flat)
   double* const buf1 = buf0 + S;
   unsigned long long* slot = (unsigned long long*)(buf1 + S);
@@ -1323,6 +1324,7 @@ __global__ void __launch_bounds__(1024) bellman_numpy_order_kernel(SoftArgs a) {
   const double* rw = a.reward + (size_t)b * S;
   for (int s = tid; s < S; s += nt) buf0[s] = v0;
   if (tid < 3) slot[tid] = 0ull;
+  if (SOFT) np_stage_tables(npt);  // numpy exp / log tables in LDS (common.h)
   __syncthreads();
   long long it = 0;
   int r3 = 0;
@@ -1337,7 +1339,7 @@ __global__ void __launch_bounds__(1024) bellman_numpy_order_kernel(SoftArgs a) {
       for (int act = 0; act < A; ++act) {
         const double dot = np_row_dot<LAYOUT>(m, b, act, s, vin);
         if (SOFT) {
-          v = softmax2(v, __dadd_rn(r, __dmul_rn(a.discount, dot)));  // maxent.py:329-333
+          v = softmax2(v, __dadd_rn(r, __dmul_rn(a.discount, dot)), npt);  // maxent.py:329-333
         } else {
           const double q = __dmul_rn(a.discount, dot);  // solver.py:44
           if (a.average) v = act == 0 ? q : __dadd_rn(v, q);
@@ -1366,7 +1368,7 @@ __global__ void __launch_bounds__(1024) bellman_numpy_order_kernel(SoftArgs a) {
     if (SOFT)
       for (int act = 0; act < A; ++act) {
         const double q = __dadd_rn(rw[s], __dmul_rn(a.discount, np_row_dot<LAYOUT>(m, b, act, s, vold)));
-        a.pi[((size_t)b * S + s) * A + act] = np_exp(q - vnew[s]);  // maxent.py:341
+        a.pi[((size_t)b * S + s) * A + act] = np_exp(q - vnew[s], npt);  // maxent.py:341
       }
   }
   if (tid == 0) {
@@ -1383,6 +1385,7 @@ __global__ void __launch_bounds__(kNpCachedThreads) bellman_numpy_order_cached_k
   const Model& m = a.m;
   const int S = m.S, A = m.A, m1 = S & ~3;
   const int b = blockIdx.x, tid = threadIdx.x, nt = blockDim.x;
+  __shared__ double npt[kNpTabLen];
   double* const buf0 = (double*)smem;  // (two named LDS pointers, not an array: ds_* accesses, not flat)
   double* const buf1 = buf0 + S;
   unsigned long long* slot = (unsigned long long*)(buf1 + S);
@@ -1398,6 +1401,7 @@ __global__ void __launch_bounds__(kNpCachedThreads) bellman_numpy_order_cached_k
   }
   for (int s = tid; s < S; s += nt) buf0[s] = v0;
   if (tid < 3) slot[tid] = 0ull;
+  if (SOFT) np_stage_tables(npt);  // numpy exp / log tables in LDS (common.h)
   __syncthreads();
   // convergence deferred over blocks of sweeps, replay of the stopping block
   // (run_deferred: the stop after the first sweep whose max|v_new - v| is not
@@ -1418,7 +1422,7 @@ __global__ void __launch_bounds__(kNpCachedThreads) bellman_numpy_order_cached_k
         if (act >= A) break;
         const double dot = rows.dot(j, act, s < m1, x);
         if (SOFT) {
-          v = softmax2(v, __dadd_rn(rr[j], __dmul_rn(a.discount, dot)));  // maxent.py:329-333
+          v = softmax2(v, __dadd_rn(rr[j], __dmul_rn(a.discount, dot)), npt);  // maxent.py:329-333
         } else {
           const double q = __dmul_rn(a.discount, dot);  // solver.py:44
           if (a.average) v = act == 0 ? q : __dadd_rn(v, q);
@@ -1465,7 +1469,7 @@ __global__ void __launch_bounds__(kNpCachedThreads) bellman_numpy_order_cached_k
       for (int act = 0; act < kNpCachedMaxActions; ++act) {
         if (act >= A) break;
         const double q = __dadd_rn(rr[j], __dmul_rn(a.discount, rows.dot(j, act, s < m1, x)));
-        a.pi[((size_t)b * S + s) * A + act] = np_exp(q - vnew[s]);  // maxent.py:341
+        a.pi[((size_t)b * S + s) * A + act] = np_exp(q - vnew[s], npt);  // maxent.py:341
       }
     }
   }
@@ -1719,6 +1723,8 @@ __global__ void __launch_bounds__(kGridThreads) bellman_grid_kernel(SoftArgs a, 
     lin = il * g.bpi + kk % g.bpi;
   }
   const int b = lin / g.bpi, blk = lin % g.bpi, tid = threadIdx.x;
+  __shared__ double npt[kNpTabLen];
+  if (SOFT) np_stage_tables(npt);  // numpy exp / log tables in LDS (common.h); grid_coresident synchronises
   if (!grid_coresident(g)) return;
   constexpr int K = KMAX;
   __shared__ unsigned long long red_in[kGridThreads / kWave], red_out[kGridThreads / kWave];
@@ -1838,7 +1844,7 @@ __global__ void __launch_bounds__(kGridThreads) bellman_grid_kernel(SoftArgs a, 
           if (kk < Kr) dot = fma(w[j][act][kk], nv[j][kk], dot);
         if (SOFT) {
           q[j][act] = __dadd_rn(r[j], __dmul_rn(a.discount, dot));
-          v = softmax2(v, q[j][act]);  // maxent.py:329-333
+          v = softmax2(v, q[j][act], npt);  // maxent.py:329-333
         } else {
           const double qq = __dmul_rn(a.discount, dot);  // solver.py:44
           if (a.average) v = act == 0 ? qq : __dadd_rn(v, qq);
@@ -1869,7 +1875,7 @@ __global__ void __launch_bounds__(kGridThreads) bellman_grid_kernel(SoftArgs a, 
     const size_t o = (size_t)b * S + sidx[j];
     if (a.value) a.value[o] = cur[j];
     if (SOFT)
-      for (int act = 0; act < A; ++act) a.pi[o * A + act] = np_exp(q[j][act] - cur[j]);  // maxent.py:341
+      for (int act = 0; act < A; ++act) a.pi[o * A + act] = np_exp(q[j][act] - cur[j], npt);  // maxent.py:341
   }
   if (blk == 0 && tid == 0) {
     if (a.iters) a.iters[b] = k;

@@ -337,7 +337,11 @@ static const unsigned kRcpSteps[16] = {1039u, 3223u, 5556u, 8048u, 10726u, 13603
                                        23705u, 27669u, 32007u, 36764u, 42010u, 47824u, 54300u, 61568u};
 
 static double np_exp1(double x) {
-  if (!(fabs(x) < 0x1.61da04cbafe44p+9)) return exp(x);
+  if (!(fabs(x) < 0x1.61da04cbafe44p+9)) {
+    if (x <= -746.0) return 0.0;
+    if (x >= 710.0) return INFINITY;
+    return exp(x);
+  }
   const double shift = 0x1.8000000003ff0p+48, inv_ln2 = 0x1.71547652b82fep+0;
   double xs = fma(x, inv_ln2, shift);
   if (fma(x, inv_ln2, shift - xs) < 0.0) xs -= 0x1p-4;
