@@ -95,15 +95,21 @@ __device__ inline double np_minimum(double a, double b) {
 // |x| >= 707.7, NaN; log: x <= 0, inf, NaN) uses ocml, which agrees with it
 // except in the last bit of some results below 1e-307 or above 1e307.
 // ---------------------------------------------------------------------------
-// The four 16-entry tables in one array (kernels with a hot soft-VI loop stage
-// it in LDS, np_stage_tables, and pass that copy: a divergent table read is then
-// an LDS read instead of a global one on the sweep's dependency chain):
+// The tables (kernels with a hot soft-VI loop stage them in LDS,
+// np_stage_tables, and pass that copy: a divergent table read is then an LDS
+// read instead of a global one on the sweep's dependency chain).  d[]:
 //   [0, 16)  exp: 2^(j/16) as a double       [16, 32) exp: its rounding error
 //   [32, 48) log: -log(R) high part          [48, 64) log: -log(R) low part
 // for the 5-bit reciprocal R of the mantissa, indexed by R's top four mantissa
 // bits (R < 0.75 folds a factor 2 into the exponent).
-constexpr int kNpTabLen = 64;
-static __constant__ double kNpTab[kNpTabLen] = {
+struct NpTables {
+  double d[64];
+  // log's reciprocal: bucket u >> 8 of the 16-bit mantissa prefix u holds
+  // (#thresholds below the bucket) | (offset of the one threshold inside it,
+  // or 256) << 8 -- the same function as the 16 compares (tests/test_npmath.py)
+  unsigned rcp[256];
+};
+static __constant__ NpTables kNpTabs = {{
     0x1.0000000000000p+0, 0x1.0b5586cf9890fp+0, 0x1.172b83c7d517bp+0, 0x1.2387a6e756238p+0,
     0x1.306fe0a31b715p+0, 0x1.3dea64c123422p+0, 0x1.4bfdad5362a27p+0, 0x1.5ab07dd485429p+0,
     0x1.6a09e667f3bcdp+0, 0x1.7a11473eb0187p+0, 0x1.8ace5422aa0dbp+0, 0x1.9c49182a3f090p+0,
@@ -119,15 +125,35 @@ static __constant__ double kNpTab[kNpTabLen] = {
     0x0.0p+0, 0x1.3ab33d066d1d2p-42, 0x1.a342c2af0003cp-45, -0x1.3d3c873e20a07p-43,
     -0x1.a21ac25d81ef3p-43, 0x1.9f1fc63382a8fp-42, -0x1.ec27d0b7b37b3p-42, -0x1.0069ce24c53fbp-42,
     0x1.b92783beb7677p-42, 0x1.9bcbecca0cdf3p-42, -0x1.30e486a0ac42dp-42, 0x1.ed8fdc149767ep-42,
-    -0x1.b8421cc74be04p-43, 0x1.2622b8757a8fbp-42, 0x1.d034451fecdfbp-43, -0x1.77771fd187145p-42};
+    -0x1.b8421cc74be04p-43, 0x1.2622b8757a8fbp-42, 0x1.d034451fecdfbp-43, -0x1.77771fd187145p-42},
+   {
+    0x10000u, 0x10000u, 0x10000u, 0x10000u, 0x00f00u, 0x10001u, 0x10001u, 0x10001u, 0x10001u, 0x10001u, 0x10001u, 0x10001u, 0x09701u, 0x10002u, 0x10002u, 0x10002u,
+    0x10002u, 0x10002u, 0x10002u, 0x10002u, 0x10002u, 0x0b402u, 0x10003u, 0x10003u, 0x10003u, 0x10003u, 0x10003u, 0x10003u, 0x10003u, 0x10003u, 0x10003u, 0x07003u,
+    0x10004u, 0x10004u, 0x10004u, 0x10004u, 0x10004u, 0x10004u, 0x10004u, 0x10004u, 0x10004u, 0x0e604u, 0x10005u, 0x10005u, 0x10005u, 0x10005u, 0x10005u, 0x10005u,
+    0x10005u, 0x10005u, 0x10005u, 0x10005u, 0x10005u, 0x02305u, 0x10006u, 0x10006u, 0x10006u, 0x10006u, 0x10006u, 0x10006u, 0x10006u, 0x10006u, 0x10006u, 0x10006u,
+    0x10006u, 0x04306u, 0x10007u, 0x10007u, 0x10007u, 0x10007u, 0x10007u, 0x10007u, 0x10007u, 0x10007u, 0x10007u, 0x10007u, 0x10007u, 0x10007u, 0x05f07u, 0x10008u,
+    0x10008u, 0x10008u, 0x10008u, 0x10008u, 0x10008u, 0x10008u, 0x10008u, 0x10008u, 0x10008u, 0x10008u, 0x10008u, 0x10008u, 0x09908u, 0x10009u, 0x10009u, 0x10009u,
+    0x10009u, 0x10009u, 0x10009u, 0x10009u, 0x10009u, 0x10009u, 0x10009u, 0x10009u, 0x10009u, 0x10009u, 0x10009u, 0x10009u, 0x01509u, 0x1000au, 0x1000au, 0x1000au,
+    0x1000au, 0x1000au, 0x1000au, 0x1000au, 0x1000au, 0x1000au, 0x1000au, 0x1000au, 0x1000au, 0x1000au, 0x1000au, 0x1000au, 0x1000au, 0x0070au, 0x1000bu, 0x1000bu,
+    0x1000bu, 0x1000bu, 0x1000bu, 0x1000bu, 0x1000bu, 0x1000bu, 0x1000bu, 0x1000bu, 0x1000bu, 0x1000bu, 0x1000bu, 0x1000bu, 0x1000bu, 0x1000bu, 0x1000bu, 0x09c0bu,
+    0x1000cu, 0x1000cu, 0x1000cu, 0x1000cu, 0x1000cu, 0x1000cu, 0x1000cu, 0x1000cu, 0x1000cu, 0x1000cu, 0x1000cu, 0x1000cu, 0x1000cu, 0x1000cu, 0x1000cu, 0x1000cu,
+    0x1000cu, 0x1000cu, 0x1000cu, 0x1000cu, 0x01a0cu, 0x1000du, 0x1000du, 0x1000du, 0x1000du, 0x1000du, 0x1000du, 0x1000du, 0x1000du, 0x1000du, 0x1000du, 0x1000du,
+    0x1000du, 0x1000du, 0x1000du, 0x1000du, 0x1000du, 0x1000du, 0x1000du, 0x1000du, 0x1000du, 0x1000du, 0x0d00du, 0x1000eu, 0x1000eu, 0x1000eu, 0x1000eu, 0x1000eu,
+    0x1000eu, 0x1000eu, 0x1000eu, 0x1000eu, 0x1000eu, 0x1000eu, 0x1000eu, 0x1000eu, 0x1000eu, 0x1000eu, 0x1000eu, 0x1000eu, 0x1000eu, 0x1000eu, 0x1000eu, 0x1000eu,
+    0x1000eu, 0x1000eu, 0x1000eu, 0x1000eu, 0x01c0eu, 0x1000fu, 0x1000fu, 0x1000fu, 0x1000fu, 0x1000fu, 0x1000fu, 0x1000fu, 0x1000fu, 0x1000fu, 0x1000fu, 0x1000fu,
+    0x1000fu, 0x1000fu, 0x1000fu, 0x1000fu, 0x1000fu, 0x1000fu, 0x1000fu, 0x1000fu, 0x1000fu, 0x1000fu, 0x1000fu, 0x1000fu, 0x1000fu, 0x1000fu, 0x1000fu, 0x1000fu,
+    0x0800fu, 0x10010u, 0x10010u, 0x10010u, 0x10010u, 0x10010u, 0x10010u, 0x10010u, 0x10010u, 0x10010u, 0x10010u, 0x10010u, 0x10010u, 0x10010u, 0x10010u, 0x10010u,
+   }};
 
-// Copy the tables into the workgroup's LDS array `t` (threads 0..63; the caller
-// synchronises before the first use).
-__device__ inline void np_stage_tables(double* t) {
-  if (threadIdx.x < kNpTabLen) t[threadIdx.x] = kNpTab[threadIdx.x];
+// Copy the tables into the workgroup's LDS copy `t` (the caller synchronises
+// before the first use).
+__device__ inline void np_stage_tables(NpTables* t) {
+  for (int i = threadIdx.x; i < 64; i += blockDim.x) t->d[i] = kNpTabs.d[i];
+  for (int i = threadIdx.x; i < 256; i += blockDim.x) t->rcp[i] = kNpTabs.rcp[i];
 }
 
-__device__ inline double np_exp(double x, const double* t = kNpTab) {
+__device__ inline double np_exp(double x, const NpTables* tt = &kNpTabs) {
+  const double* t = tt->d;
   if (!(fabs(x) < 0x1.61da04cbafe44p+9)) {  // SVML's rare path
     if (x <= -746.0) return 0.0;            // underflow (-inf: soft VI's first softmax of a non-terminal state)
     if (x >= 710.0) return (double)INFINITY;
@@ -155,7 +181,14 @@ __device__ inline double np_exp(double x, const double* t = kNpTab) {
   return ldexp(q, (int)floor(n));
 }
 
-__device__ inline double np_log(double x, const double* t = kNpTab) {
+// `bucket`: count the reciprocal's thresholds with one read of the 256-bucket
+// table in LDS (shortest dependency chain: the single-instance grid shape and
+// the numpy-order kernels) or with 16 compares (the default: no extra table
+// access; grids with several states per thread, where
+// the measured soft VI at 64 instances ran 46 ms with compares, 55 with the
+// bucket read; tools/diag/soft_ab.py).  Same result either way.
+__device__ inline double np_log(double x, const NpTables* tt = &kNpTabs, bool bucket = false) {
+  const double* t = tt->d;
   if (!(x > 0.0) || isinf(x)) return log(x);  // rare path: 0, negative, inf, NaN
   int e;
   const double m = ldexp(frexp(x, &e), 1);  // [1, 2): getmant; e - 1 = getexp
@@ -165,11 +198,17 @@ __device__ inline double np_log(double x, const double* t = kNpTab) {
   // all 65,536 u on an AVX-512 host: tools/gen_npmath.py).  Summed as a tree
   // (independent compares, three levels of adds): it is on the dependency chain.
   const unsigned u = (unsigned)(__double_as_longlong(m) >> 36) & 0xffffu;
-  const int n0 = ((u >= 1039u) + (u >= 3223u)) + ((u >= 5556u) + (u >= 8048u));
-  const int n1 = ((u >= 10726u) + (u >= 13603u)) + ((u >= 16707u) + (u >= 20063u));
-  const int n2 = ((u >= 23705u) + (u >= 27669u)) + ((u >= 32007u) + (u >= 36764u));
-  const int n3 = ((u >= 42010u) + (u >= 47824u)) + ((u >= 54300u) + (u >= 61568u));
-  const int nd = (n0 + n1) + (n2 + n3);
+  int nd;
+  if (bucket) {
+    const unsigned be = tt->rcp[u >> 8];
+    nd = (int)(be & 0xffu) + ((u & 0xffu) >= (be >> 8) ? 1 : 0);
+  } else {
+    const int n0 = ((u >= 1039u) + (u >= 3223u)) + ((u >= 5556u) + (u >= 8048u));
+    const int n1 = ((u >= 10726u) + (u >= 13603u)) + ((u >= 16707u) + (u >= 20063u));
+    const int n2 = ((u >= 23705u) + (u >= 27669u)) + ((u >= 32007u) + (u >= 36764u));
+    const int n3 = ((u >= 42010u) + (u >= 47824u)) + ((u >= 54300u) + (u >= 61568u));
+    nd = (n0 + n1) + (n2 + n3);
+  }
   const int idx = (16 - nd) & 15;
   const double th = t[32 + idx], tl = t[48 + idx];
   const double R = (double)(32 - nd) * 0x1p-5;
@@ -195,10 +234,10 @@ __device__ inline double np_log(double x, const double* t = kNpTab) {
 // maxent.py:260-276 -- max + log(1 + exp(min - max)) with numpy's exp / log;
 // the log(1+exp) form (not log1p) is kept deliberately so rounding follows
 // the reference.
-__device__ inline double softmax2(double x1, double x2, const double* t = kNpTab) {
+__device__ inline double softmax2(double x1, double x2, const NpTables* t = &kNpTabs, bool bucket = false) {
   const double hi = np_maximum(x1, x2);
   const double lo = np_minimum(x1, x2);
-  return __dadd_rn(hi, np_log(__dadd_rn(1.0, np_exp(__dsub_rn(lo, hi), t)), t));
+  return __dadd_rn(hi, np_log(__dadd_rn(1.0, np_exp(__dsub_rn(lo, hi), t)), t, bucket));
 }
 
 // ---------------------------------------------------------------------------

@@ -1316,7 +1316,8 @@ __global__ void __launch_bounds__(1024) bellman_numpy_order_kernel(SoftArgs a) {
   const Model& m = a.m;
   const int S = m.S, A = m.A;
   const int b = blockIdx.x, tid = threadIdx.x, nt = blockDim.x;
-  __shared__ double npt[kNpTabLen];
+  __shared__ NpTables npt_lds;
+  const NpTables* const npt = &npt_lds;
   double* const buf0 = (double*)smem;  // (two named LDS pointers, not an array: ds_* accesses, not flat)
   double* const buf1 = buf0 + S;
   unsigned long long* slot = (unsigned long long*)(buf1 + S);
@@ -1324,7 +1325,7 @@ __global__ void __launch_bounds__(1024) bellman_numpy_order_kernel(SoftArgs a) {
   const double* rw = a.reward + (size_t)b * S;
   for (int s = tid; s < S; s += nt) buf0[s] = v0;
   if (tid < 3) slot[tid] = 0ull;
-  if (SOFT) np_stage_tables(npt);  // numpy exp / log tables in LDS (common.h)
+  if (SOFT) np_stage_tables(&npt_lds);  // numpy exp / log tables in LDS (common.h)
   __syncthreads();
   long long it = 0;
   int r3 = 0;
@@ -1339,7 +1340,7 @@ __global__ void __launch_bounds__(1024) bellman_numpy_order_kernel(SoftArgs a) {
       for (int act = 0; act < A; ++act) {
         const double dot = np_row_dot<LAYOUT>(m, b, act, s, vin);
         if (SOFT) {
-          v = softmax2(v, __dadd_rn(r, __dmul_rn(a.discount, dot)), npt);  // maxent.py:329-333
+          v = softmax2(v, __dadd_rn(r, __dmul_rn(a.discount, dot)), npt, true);  // maxent.py:329-333
         } else {
           const double q = __dmul_rn(a.discount, dot);  // solver.py:44
           if (a.average) v = act == 0 ? q : __dadd_rn(v, q);
@@ -1385,7 +1386,8 @@ __global__ void __launch_bounds__(kNpCachedThreads) bellman_numpy_order_cached_k
   const Model& m = a.m;
   const int S = m.S, A = m.A, m1 = S & ~3;
   const int b = blockIdx.x, tid = threadIdx.x, nt = blockDim.x;
-  __shared__ double npt[kNpTabLen];
+  __shared__ NpTables npt_lds;
+  const NpTables* const npt = &npt_lds;
   double* const buf0 = (double*)smem;  // (two named LDS pointers, not an array: ds_* accesses, not flat)
   double* const buf1 = buf0 + S;
   unsigned long long* slot = (unsigned long long*)(buf1 + S);
@@ -1401,7 +1403,7 @@ __global__ void __launch_bounds__(kNpCachedThreads) bellman_numpy_order_cached_k
   }
   for (int s = tid; s < S; s += nt) buf0[s] = v0;
   if (tid < 3) slot[tid] = 0ull;
-  if (SOFT) np_stage_tables(npt);  // numpy exp / log tables in LDS (common.h)
+  if (SOFT) np_stage_tables(&npt_lds);  // numpy exp / log tables in LDS (common.h)
   __syncthreads();
   // convergence deferred over blocks of sweeps, replay of the stopping block
   // (run_deferred: the stop after the first sweep whose max|v_new - v| is not
@@ -1422,7 +1424,7 @@ __global__ void __launch_bounds__(kNpCachedThreads) bellman_numpy_order_cached_k
         if (act >= A) break;
         const double dot = rows.dot(j, act, s < m1, x);
         if (SOFT) {
-          v = softmax2(v, __dadd_rn(rr[j], __dmul_rn(a.discount, dot)), npt);  // maxent.py:329-333
+          v = softmax2(v, __dadd_rn(rr[j], __dmul_rn(a.discount, dot)), npt, true);  // maxent.py:329-333
         } else {
           const double q = __dmul_rn(a.discount, dot);  // solver.py:44
           if (a.average) v = act == 0 ? q : __dadd_rn(v, q);
@@ -1723,8 +1725,9 @@ __global__ void __launch_bounds__(kGridThreads) bellman_grid_kernel(SoftArgs a, 
     lin = il * g.bpi + kk % g.bpi;
   }
   const int b = lin / g.bpi, blk = lin % g.bpi, tid = threadIdx.x;
-  __shared__ double npt[kNpTabLen];
-  if (SOFT) np_stage_tables(npt);  // numpy exp / log tables in LDS (common.h); grid_coresident synchronises
+  __shared__ NpTables npt_lds;
+  const NpTables* const npt = &npt_lds;
+  if (SOFT) np_stage_tables(&npt_lds);  // numpy exp / log tables in LDS (common.h); grid_coresident synchronises
   if (!grid_coresident(g)) return;
   constexpr int K = KMAX;
   __shared__ unsigned long long red_in[kGridThreads / kWave], red_out[kGridThreads / kWave];
@@ -1844,7 +1847,7 @@ __global__ void __launch_bounds__(kGridThreads) bellman_grid_kernel(SoftArgs a, 
           if (kk < Kr) dot = fma(w[j][act][kk], nv[j][kk], dot);
         if (SOFT) {
           q[j][act] = __dadd_rn(r[j], __dmul_rn(a.discount, dot));
-          v = softmax2(v, q[j][act], npt);  // maxent.py:329-333
+          v = softmax2(v, q[j][act], npt, SPT == 1);  // maxent.py:329-333
         } else {
           const double qq = __dmul_rn(a.discount, dot);  // solver.py:44
           if (a.average) v = act == 0 ? qq : __dadd_rn(v, qq);

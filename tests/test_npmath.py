@@ -86,6 +86,21 @@ def test_rcp_thresholds_in_sources():
     assert [int(t) for t in re.findall(r"(\d+)u", body)] == steps
 
 
+def test_rcp_bucket_table_equals_thresholds():
+    """The device's default reciprocal count (IRLMX_NPMATH_BUCKET: one 256-entry
+    table read) is the 16-threshold count for every 16-bit mantissa prefix."""
+    dev = open(os.path.join(ROOT, "irl-maxent_amd", "csrc", "common.h")).read()
+    body = dev[dev.index("unsigned rcp[256];"):]
+    body = body[body.index("{{"):body.index("}};")]
+    ent = [int(t, 16) for t in re.findall(r"0x([0-9a-f]+)u", body.split("},")[-1])]
+    assert len(ent) == 256
+    steps = np.array([int(t) for t in Z["rcp_steps"]])
+    u = np.arange(65536)
+    e = np.array(ent)[u >> 8]
+    nd = (e & 0xFF) + ((u & 255) >= (e >> 8))
+    assert np.array_equal(nd, (u[:, None] >= steps[None, :]).sum(axis=1))
+
+
 def test_numpy_math_arguments():
     import irlmx._lib as L
     lib = L.load()
