@@ -219,6 +219,10 @@ static void error_paths() {
   expect(irlmx_execution_plan(&good, IRLMX_OP_FORWARD, nullptr), IRLMX_EINVAL, "plan is NULL", "null plan");
   expect(irlmx_mdp_properties(nullptr, (int32_t*)f, nullptr), IRLMX_EINVAL, "mdp is NULL", "props null mdp");
   expect(irlmx_mdp_properties(&good, nullptr, nullptr), IRLMX_EINVAL, "props is NULL", "props null out");
+  expect(irlmx_numpy_math(2, (double*)f, (double*)f, 4, nullptr), IRLMX_EINVAL, "unknown op 2", "npmath op");
+  expect(irlmx_numpy_math(IRLMX_NPMATH_EXP, (double*)f, (double*)f, -1, nullptr), IRLMX_EINVAL, "< 0", "npmath n");
+  expect(irlmx_numpy_math(IRLMX_NPMATH_LOG, nullptr, (double*)f, 4, nullptr), IRLMX_EINVAL, "NULL", "npmath null");
+  expect(irlmx_numpy_math(IRLMX_NPMATH_EXP, nullptr, nullptr, 0, nullptr), IRLMX_OK, "", "npmath empty");
   expect(irlmx_build_icy_gridworld(0, (double*)f, 1, (double*)f, nullptr), IRLMX_EINVAL, "size=0", "icy size");
   expect(irlmx_build_gridworld(50000, 1, (double*)f, nullptr), IRLMX_EINVAL, "size=50000", "grid size");
   expect(irlmx_dense_to_stencil((double*)f, 5, 5, 4, (double*)f, nullptr, nullptr), IRLMX_EINVAL, "off_stencil NULL",
